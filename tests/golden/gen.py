@@ -1,0 +1,167 @@
+"""Deterministic fixture generator shared by ``make_golden.py`` and the tests.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in ``td3_amd/`` imports this module.
+
+The reference initialises its networks with torch's default init
+(``torch/nn/modules/linear.py:117-128``: kaiming-uniform(a=sqrt 5) for the
+weight == U(+-1/sqrt(fan_in)); bias U(+-1/sqrt(fan_in)); LayerNorm gamma=1,
+beta=0).  Reproducing torch's RNG stream is pointless, so fixtures use this
+small documented generator instead and *load* the result into the reference
+(``load_state_dict``) when the goldens are made:
+
+* Linear / Conv weight   ~ U(-1/sqrt(fan_in), +1/sqrt(fan_in))
+* Linear / Conv bias     ~ U(-1/sqrt(fan_in), +1/sqrt(fan_in))   (fan_in of its weight)
+* LayerNorm weight       ~ U(0.8, 1.2)      (randomised so the LN affine path is exercised)
+* LayerNorm bias         ~ U(-0.1, 0.1)
+
+drawn in ``state_dict`` order from ``numpy.random.RandomState(seed)`` and cast
+to float32.  Replay contents are drawn from ``RandomState(seed + 1)``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ACTOR_ARCH = (500, 400, 300)      # TD3_featured.py:19, TD3_particles.py:25
+Q_ARCH = (500, 400, 200)          # TD3_featured.py:54
+QP_ARCH = (500, 400, 300)         # TD3_particles.py:76
+NUM_FEATURES = 128                # TD3_particles.py:27
+
+
+def _mlp_shapes(prefix, in_dim, arch, out_dim, norm, first_norm_dim=None):
+    shapes = []
+    dims = [in_dim] + list(arch)
+    for i, d in enumerate(arch):
+        shapes.append((f"{prefix}linears.{i}.weight", (d, dims[i])))
+        shapes.append((f"{prefix}linears.{i}.bias", (d,)))
+    shapes.append((f"{prefix}linears.{len(arch)}.weight", (out_dim, arch[-1])))
+    shapes.append((f"{prefix}linears.{len(arch)}.bias", (out_dim,)))
+    if norm == "layer":
+        if first_norm_dim is not None:
+            shapes.append((f"{prefix}lnorm1.weight", (first_norm_dim,)))
+            shapes.append((f"{prefix}lnorm1.bias", (first_norm_dim,)))
+        for i, d in enumerate(arch):
+            shapes.append((f"{prefix}lnorms.{i}.weight", (d,)))
+            shapes.append((f"{prefix}lnorms.{i}.bias", (d,)))
+    return shapes
+
+
+def featured_actor_shapes(sd, ad, norm):
+    """State-dict order of ``TD3_featured.Actor`` (TD3_featured.py:15-36)."""
+    return _mlp_shapes("", sd, ACTOR_ARCH, ad, norm)
+
+
+def featured_critic_shapes(sd, ad, norm):
+    """State-dict order of ``TD3_featured.Critic`` (q1.* then q2.*, TD3_featured.py:84-89)."""
+    out = []
+    for q in ("q1.", "q2."):
+        out += _mlp_shapes(q, sd + ad, Q_ARCH, 1, norm)
+    return out
+
+
+def _encoder_shapes(prefix, D):
+    f2 = NUM_FEATURES * 2
+    return [
+        (f"{prefix}conv1.weight", (f2, 1, 1, D)),
+        (f"{prefix}conv1.bias", (f2,)),
+        (f"{prefix}conv2.weight", (NUM_FEATURES, f2, 1)),
+        (f"{prefix}conv2.bias", (NUM_FEATURES,)),
+    ]
+
+
+def particle_actor_shapes(F, D, A, norm):
+    """State-dict order of ``TD3_particles.Actor`` (TD3_particles.py:19-50)."""
+    inp = NUM_FEATURES + F
+    return _encoder_shapes("", D) + _mlp_shapes("", inp, ACTOR_ARCH, A, norm, first_norm_dim=inp)
+
+
+def particle_critic_shapes(F, D, A, norm, cdq=True):
+    """State-dict order of ``TD3_particles.Critic`` (TD3_particles.py:121-128)."""
+    inp = NUM_FEATURES + F + A
+    out = []
+    for q in (("q1.", "q2.") if cdq else ("q1.",)):
+        out += _encoder_shapes(q, D) + _mlp_shapes(q, inp, QP_ARCH, A, norm, first_norm_dim=inp)
+    return out
+
+
+def init_params(shapes, seed):
+    """Draw every tensor of ``shapes`` (state-dict order) from RandomState(seed)."""
+    rs = np.random.RandomState(seed)
+    out = {}
+    fan_in = None
+    for name, shape in shapes:
+        if "lnorm" in name:
+            if name.endswith("weight"):
+                v = rs.uniform(0.8, 1.2, size=shape)
+            else:
+                v = rs.uniform(-0.1, 0.1, size=shape)
+        elif name.endswith("weight"):
+            fan_in = int(np.prod(shape[1:]))
+            bound = 1.0 / np.sqrt(fan_in)
+            v = rs.uniform(-bound, bound, size=shape)
+        else:
+            bound = 1.0 / np.sqrt(fan_in)
+            v = rs.uniform(-bound, bound, size=shape)
+        out[name] = v.astype(np.float32)
+    return out
+
+
+def fill_featured_buffer(sd, ad, max_action, n, seed):
+    """Transitions as the env would hand them to ``ReplayBuffer.add`` (float64)."""
+    rs = np.random.RandomState(seed + 1)
+    state = rs.standard_normal((n, sd))
+    action = rs.uniform(-max_action, max_action, size=(n, ad))
+    next_state = rs.standard_normal((n, sd))
+    reward = rs.standard_normal((n,))
+    done = (rs.uniform(size=(n,)) < 0.01).astype(np.float64)
+    return state, action, next_state, reward, done
+
+
+def fill_particle_buffer(F, N, D, A, n, seed):
+    rs = np.random.RandomState(seed + 1)
+    feat = rs.standard_normal((n, F))
+    part = rs.standard_normal((n, N, D))
+    action = rs.uniform(-1.0, 1.0, size=(n, A))
+    next_feat = rs.standard_normal((n, F))
+    next_part = rs.standard_normal((n, N, D))
+    reward = rs.standard_normal((n,))
+    done = (rs.uniform(size=(n,)) < 0.01).astype(np.float64)
+    return feat, part, action, next_feat, next_part, reward, done
+
+
+def sample_positions(numel, k=512, salt=0):
+    """Fixed element positions at which fixtures keep exact values of a tensor."""
+    rs = np.random.RandomState(1234 + salt)
+    if numel <= k:
+        return np.arange(numel)
+    return np.sort(rs.choice(numel, size=k, replace=False))
+
+
+def summarize(arr, salt=0):
+    """(sum, sum of squares, max |x|, samples) of a float32 tensor, sums in float64."""
+    a = np.asarray(arr, dtype=np.float32).reshape(-1)
+    pos = sample_positions(a.size, salt=salt)
+    a64 = a.astype(np.float64)
+    return np.array([a64.sum(), (a64 * a64).sum(), np.abs(a64).max()]), a[pos].copy()
+
+
+FEATURED_CONFIGS = {
+    # name: (sd, ad, max_action, norm, batch, steps, hyper-params)
+    "pend_layer": (3, 1, 2.0, "layer", 256, 4, {}),
+    "hc_layer": (17, 6, 1.0, "layer", 256, 4, {}),
+    "hc_none": (17, 6, 1.0, None, 256, 4, {}),
+    "hc_layer_b100": (17, 6, 1.0, "layer", 100, 2, {}),
+    "hc_layer_hp": (17, 6, 1.0, "layer", 64, 3,
+                    dict(discount=0.999, tau=0.01, lr=3e-4, policy_freq=3,
+                         policy_noise=0.3, noise_clip=0.4)),
+    "hum_layer": (376, 17, 0.4, "layer", 128, 2, {}),
+}
+
+PARTICLE_CONFIGS = {
+    # name: (F, N, D, A, norm, cdq, batch, steps)
+    "part_layer": (7, 16, 9, 3, "layer", True, 32, 2),
+    "part_nocdq": (7, 16, 9, 3, "layer", False, 32, 2),
+    "part_none": (7, 16, 9, 3, None, True, 32, 2),
+}
+
+BUFFER_ROWS = 1000
+SEED = 7

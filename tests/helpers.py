@@ -1,0 +1,72 @@
+"""Shared test helpers: golden loading, oracle driving, tolerance checks."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, GOLDEN):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import gen  # noqa: E402
+from oracle import td3_oracle as orc  # noqa: E402
+
+# Tolerances (fp32): forward values / losses rtol 1e-5 atol 1e-6,
+# gradients rtol 1e-4 atol 1e-7, post-Adam params atol 2*lr on <=0.1% of elements.
+FWD_RTOL, FWD_ATOL = 1e-5, 1e-6
+GRAD_RTOL, GRAD_ATOL = 1e-4, 1e-7
+
+
+def load_golden(kind, name):
+    return dict(np.load(os.path.join(GOLDEN, f"{kind}_{name}.npz"), allow_pickle=False))
+
+
+def featured_setup(name):
+    sd, ad, ma, norm, B, steps, hp = gen.FEATURED_CONFIGS[name]
+    a0 = gen.init_params(gen.featured_actor_shapes(sd, ad, norm), gen.SEED)
+    c0 = gen.init_params(gen.featured_critic_shapes(sd, ad, norm), gen.SEED + 100)
+    buf = orc.FeaturedBuffer(sd, ad, gen.BUFFER_ROWS)
+    s, a, s2, r, d = gen.fill_featured_buffer(sd, ad, ma, gen.BUFFER_ROWS, gen.SEED)
+    for i in range(gen.BUFFER_ROWS):
+        buf.add(s[i], a[i], s2[i], r[i], d[i])
+    kw = dict(max_action=ma, norm=norm)
+    kw.update(hp)
+    return dict(sd=sd, ad=ad, ma=ma, norm=norm, B=B, steps=steps, hp=hp, actor=a0,
+                critic=c0, buf=buf, kw=kw)
+
+
+def particle_setup(name):
+    Fd, N, D, A, norm, cdq, B, steps = gen.PARTICLE_CONFIGS[name]
+    a0 = gen.init_params(gen.particle_actor_shapes(Fd, D, A, norm), gen.SEED)
+    c0 = gen.init_params(gen.particle_critic_shapes(Fd, D, A, norm, cdq), gen.SEED + 100)
+    buf = orc.ParticleBuffer(Fd, N, D, A, gen.BUFFER_ROWS)
+    f, p, a, f2, p2, r, d = gen.fill_particle_buffer(Fd, N, D, A, gen.BUFFER_ROWS, gen.SEED)
+    for i in range(gen.BUFFER_ROWS):
+        buf.add((f[i], p[i]), a[i], (f2[i], p2[i]), r[i], d[i])
+    return dict(F=Fd, N=N, D=D, A=A, norm=norm, cdq=cdq, B=B, steps=steps, actor=a0,
+                critic=c0, buf=buf, kw=dict(norm=norm, cdq=cdq))
+
+
+def summary_close(arr, stats, samples, salt, rtol, atol, what=""):
+    st, smp = gen.summarize(arr, salt=salt)
+    np.testing.assert_allclose(smp, samples, rtol=rtol, atol=atol, err_msg=f"{what} samples")
+    scale = max(1.0, abs(stats[0]))
+    assert abs(st[0] - stats[0]) <= 1e-4 * scale + atol * np.asarray(arr).size ** 0.5, what
+    np.testing.assert_allclose(st[1], stats[1], rtol=1e-4, atol=1e-10, err_msg=f"{what} sumsq")
+    np.testing.assert_allclose(st[2], stats[2], rtol=1e-4, atol=atol, err_msg=f"{what} maxabs")
+
+
+def params_close(P, golden, prefix, salt_base, atol, rtol=1e-5, frac_loose=1e-3, loose=2e-4):
+    """Post-Adam parameter check: tight everywhere except a tiny loose fraction."""
+    for i, (k, v) in enumerate(P.items()):
+        st, smp = gen.summarize(v, salt=salt_base + i)
+        ref = golden[f"{prefix}/{k}/samples"]
+        err = np.abs(smp - ref)
+        tol = atol + rtol * np.abs(ref)
+        bad = err > tol
+        assert bad.mean() <= frac_loose or bad.sum() <= 1, (prefix, k, bad.sum(), err.max())
+        assert err.max() <= loose, (prefix, k, err.max())
