@@ -1,0 +1,160 @@
+/*
+ * libtd3hip -- C ABI of the MI355X-native TD3 gradient step (gfx950).
+ *
+ * Plain pointers and sizes only; no torch types.  Every function returns 0 on
+ * success, -1 on an argument error and -2 on a HIP / RCCL error; the message of
+ * the last failure on the calling thread is td3_last_error().
+ *
+ * Each entry point replaces one piece of the reference's Python surface
+ * (/root/reference, duck-typed classes selected at main.py:203-208):
+ *
+ *   rb_create            ReplayBuffer_featured.__init__   my_replay_buffer.py:73-89
+ *   rb_add               ReplayBuffer_featured.add        my_replay_buffer.py:109-117
+ *   rb_sample            ReplayBuffer_featured.sample     my_replay_buffer.py:119-128
+ *   rb_read/write_records ReplayBuffer_featured.save/load my_replay_buffer.py:91-107
+ *   td3_create           TD3.__init__ + TD3_base.__init__ TD3_featured.py:100-110, TD3_base.py:7-24
+ *   td3_get/set_params   state_dict()/load_state_dict()   TD3_base.py:26-50 (save/load)
+ *   td3_train_step       TD3.train(replay_buffer, B)      TD3_featured.py:123-171
+ *   td3_train_step_batch TD3.train on a foreign buffer's sample() tensors
+ *   td3_select_action    TD3.select_action                TD3_featured.py:113-115
+ *   td3_eval_q           TD3.eval_q                       TD3_featured.py:117-121
+ *
+ * Ownership: handles own all device memory.  Host pointers are owned by the caller
+ * and only read/written during the call.  Device pointers passed in (rb_sample
+ * outputs, td3_train_step_batch inputs) must stay valid until the stream work of
+ * the call has completed.
+ *
+ * Streams: `stream` arguments are hipStream_t passed as void*; NULL selects the
+ * handle's own stream.  td3_train_step orders itself after the ring's last
+ * rb_add / rb_fill_synthetic (a transition added at step t is samplable at t,
+ * main.py:261 before :269).  Handles are not re-entrant.
+ */
+#ifndef TD3_HIP_H
+#define TD3_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rb_handle rb_handle;
+typedef struct td3_handle td3_handle;
+
+/* ------------------------------------------------------------------ replay ring */
+typedef struct rb_info_t {
+  int state_dim, action_dim;
+  int record_floats;       /* floats per HBM record: [s | a | s2 | r | not_done | pad] */
+  int64_t max_size, ptr, size;
+  void* data;              /* device pointer of the ring [max_size][record_floats] */
+  int device;
+} rb_info_t;
+
+int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint64_t seed,
+              rb_handle** out);
+int rb_destroy(rb_handle* h);
+int rb_info(const rb_handle* h, rb_info_t* info);
+/* n transitions, row-major float64 host arrays (reference dtype); stores 1-done. */
+int rb_add(rb_handle* h, const double* state, const double* action, const double* next_state,
+           const double* reward, const double* done, int64_t n, void* stream);
+/* n packed float32 records (record_floats each). */
+int rb_add_records(rb_handle* h, const float* records, int64_t n, void* stream);
+/* Device-side synthetic prefill (SURVEY.md §8d distribution), n rows at ptr. */
+int rb_fill_synthetic(rb_handle* h, int64_t n, float max_action, uint64_t seed, void* stream);
+/* Gather `batch` rows into device outputs state[B][sd], action[B][ad], next_state[B][sd],
+ * reward[B], not_done[B].  inject_idx (device, nullable) replaces the Philox draw;
+ * idx_out (device, nullable) receives the rows drawn. */
+int rb_sample(rb_handle* h, int batch, float* state, float* action, float* next_state,
+              float* reward, float* not_done, const int64_t* inject_idx, int64_t* idx_out,
+              void* stream);
+int rb_read_records(const rb_handle* h, int64_t start, int64_t n, float* out);
+int rb_write_records(rb_handle* h, int64_t start, int64_t n, const float* in, int64_t ptr,
+                     int64_t size);
+int rb_sync(rb_handle* h);
+
+/* ------------------------------------------------------------------ learner */
+typedef struct td3_config {
+  int state_dim, action_dim;
+  int actor_hidden[3];     /* reference: (500, 400, 300)  TD3_featured.py:19 */
+  int critic_hidden[3];    /* reference: (500, 400, 200)  TD3_featured.py:54 */
+  int norm;                /* 0: None, 1: "layer"  (TD3_featured.py:28-31) */
+  float max_action;
+  double discount, tau, policy_noise, noise_clip;   /* TD3_base.py:9-13 */
+  int policy_freq;
+  double lr, beta1, beta2, eps;                     /* torch.optim.Adam defaults */
+  uint64_t seed;           /* Philox key for index draws and target-policy noise */
+  int device;
+  int use_graph;           /* capture each step variant into a hipGraph (default 1) */
+} td3_config;
+
+enum td3_which {
+  TD3_ACTOR = 0, TD3_ACTOR_TARGET = 1, TD3_CRITIC = 2, TD3_CRITIC_TARGET = 3,
+  TD3_ACTOR_ADAM_M = 4, TD3_ACTOR_ADAM_V = 5, TD3_CRITIC_ADAM_M = 6, TD3_CRITIC_ADAM_V = 7
+};
+
+typedef struct td3_step_stats {
+  double critic_loss;      /* mse(Q1,y) + mse(Q2,y)  (TD3_featured.py:148) */
+  double actor_loss;       /* -mean Q1(s, pi(s)) on actor steps, else NaN (:159) */
+  int actor_step;          /* 1 when the delayed policy update ran (:156) */
+  float* y;                /* nullable host [B]: target Q */
+  float* q1;               /* nullable host [B] */
+  float* q2;               /* nullable host [B] */
+  int64_t* idx;            /* nullable host [B]: rows drawn */
+} td3_step_stats;
+
+void td3_default_config(td3_config* cfg);
+int td3_create(const td3_config* cfg, td3_handle** out);
+int td3_destroy(td3_handle* h);
+
+/* Parameter tensors in reference state_dict order (Actor: linears.{0..3}.{weight,bias},
+ * lnorms.{0..2}.{weight,bias}; Critic: q1.* then q2.*).  Flat, unpadded. */
+int td3_tensor_count(const td3_handle* h, int which_group /*0 actor, 1 critic*/);
+int td3_tensor_info(const td3_handle* h, int which_group, int index, char* name, int name_len,
+                    int64_t* rows, int64_t* cols);
+int64_t td3_num_params(const td3_handle* h, int which_group);
+int td3_get_params(td3_handle* h, int which, float* out, int64_t n);
+int td3_set_params(td3_handle* h, int which, const float* in, int64_t n);
+int td3_get_counters(const td3_handle* h, int64_t* total_it, int64_t* critic_step,
+                     int64_t* actor_step);
+int td3_set_counters(td3_handle* h, int64_t total_it, int64_t critic_step, int64_t actor_step);
+
+/* One TD3.train(rb, batch) step.  inject_idx [batch] int64 / inject_noise [batch][ad]
+ * float32 are HOST arrays (nullable) replacing the Philox draws (parity testing).
+ * stats (nullable) forces a sync and fills losses. */
+int td3_train_step(td3_handle* h, rb_handle* rb, int batch, void* stream,
+                   const int64_t* inject_idx, const float* inject_noise, td3_step_stats* stats);
+/* Same step on an already-sampled batch (device float32 pointers, contiguous). */
+int td3_train_step_batch(td3_handle* h, const float* state, const float* action,
+                         const float* next_state, const float* reward, const float* not_done,
+                         int batch, void* stream, const float* inject_noise,
+                         td3_step_stats* stats);
+/* n states (host, [n][sd]) -> n actions (host, [n][ad]); synchronous. */
+int td3_select_action(td3_handle* h, const float* state, float* action_out, int n);
+/* (state, action) (host) -> q_out[2*n] = Q1, Q2; synchronous. */
+int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_out, int n);
+
+/* ------------------------------------------------------------------ multi-GPU (RCCL) */
+int td3_comm_unique_id(unsigned char out[128]);
+/* Data-parallel mode: grads are all-reduced (sum, then /world) over RCCL before Adam. */
+int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int rank);
+
+/* ------------------------------------------------------------------ measurement */
+int td3_sync(td3_handle* h);
+void* td3_stream(td3_handle* h);
+/* Per-stage device times (ms) of one eager step; names via td3_stage_name. */
+int td3_profile_stages(td3_handle* h, rb_handle* rb, int batch, int actor_phase, float* ms,
+                       int max_stages, int* n_stages);
+const char* td3_stage_name(td3_handle* h, int i);
+/* Re-launch one stage `iters` times back-to-back between two HIP events on the
+ * handle stream (after one full step at `batch`); returns mean ms per launch. */
+int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean);
+/* Algorithmic FLOPs of one launch of stage i (MFMA stages; 0 otherwise). */
+double td3_stage_flops(td3_handle* h, int i);
+
+const char* td3_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TD3_HIP_H */

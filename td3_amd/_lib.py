@@ -1,0 +1,145 @@
+"""ctypes binding of libtd3hip.so (the C-ABI declared in include/td3.h).
+
+The library is built in-tree by ``td3_amd.build`` (hipcc, gfx950).  There is no
+fallback: if the shared object is missing or fails to load, importing the
+product modules raises -- the HIP path is the only compute path.
+"""
+from __future__ import annotations
+
+import atexit
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtd3hip.so")
+
+
+class rb_info_t(C.Structure):
+    _fields_ = [("state_dim", C.c_int), ("action_dim", C.c_int), ("record_floats", C.c_int),
+                ("max_size", C.c_int64), ("ptr", C.c_int64), ("size", C.c_int64),
+                ("data", C.c_void_p), ("device", C.c_int)]
+
+
+class td3_config(C.Structure):
+    _fields_ = [("state_dim", C.c_int), ("action_dim", C.c_int),
+                ("actor_hidden", C.c_int * 3), ("critic_hidden", C.c_int * 3),
+                ("norm", C.c_int), ("max_action", C.c_float),
+                ("discount", C.c_double), ("tau", C.c_double), ("policy_noise", C.c_double),
+                ("noise_clip", C.c_double), ("policy_freq", C.c_int),
+                ("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double),
+                ("eps", C.c_double), ("seed", C.c_uint64), ("device", C.c_int),
+                ("use_graph", C.c_int)]
+
+
+class td3_step_stats(C.Structure):
+    _fields_ = [("critic_loss", C.c_double), ("actor_loss", C.c_double), ("actor_step", C.c_int),
+                ("y", C.c_void_p), ("q1", C.c_void_p), ("q2", C.c_void_p), ("idx", C.c_void_p)]
+
+
+_P = C.c_void_p
+_F = C.POINTER(C.c_float)
+_D = C.POINTER(C.c_double)
+_I64 = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); every symbol of include/td3.h.
+SIGNATURES = {
+    "rb_create": (C.c_int, [C.c_int, C.c_int, C.c_int64, C.c_int, C.c_uint64, C.POINTER(_P)]),
+    "rb_destroy": (C.c_int, [_P]),
+    "rb_info": (C.c_int, [_P, C.POINTER(rb_info_t)]),
+    "rb_add": (C.c_int, [_P, _D, _D, _D, _D, _D, C.c_int64, _P]),
+    "rb_add_records": (C.c_int, [_P, _F, C.c_int64, _P]),
+    "rb_fill_synthetic": (C.c_int, [_P, C.c_int64, C.c_float, C.c_uint64, _P]),
+    "rb_sample": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rb_read_records": (C.c_int, [_P, C.c_int64, C.c_int64, _F]),
+    "rb_write_records": (C.c_int, [_P, C.c_int64, C.c_int64, _F, C.c_int64, C.c_int64]),
+    "rb_sync": (C.c_int, [_P]),
+    "td3_default_config": (None, [C.POINTER(td3_config)]),
+    "td3_create": (C.c_int, [C.POINTER(td3_config), C.POINTER(_P)]),
+    "td3_destroy": (C.c_int, [_P]),
+    "td3_tensor_count": (C.c_int, [_P, C.c_int]),
+    "td3_tensor_info": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p, C.c_int, _I64, _I64]),
+    "td3_num_params": (C.c_int64, [_P, C.c_int]),
+    "td3_get_params": (C.c_int, [_P, C.c_int, _F, C.c_int64]),
+    "td3_set_params": (C.c_int, [_P, C.c_int, _F, C.c_int64]),
+    "td3_get_counters": (C.c_int, [_P, _I64, _I64, _I64]),
+    "td3_set_counters": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64]),
+    "td3_train_step": (C.c_int, [_P, _P, C.c_int, _P, _I64, _F, C.POINTER(td3_step_stats)]),
+    "td3_train_step_batch": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_int, _P, _F,
+                                       C.POINTER(td3_step_stats)]),
+    "td3_select_action": (C.c_int, [_P, _F, _F, C.c_int]),
+    "td3_eval_q": (C.c_int, [_P, _F, _F, _F, C.c_int]),
+    "td3_comm_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
+    "td3_comm_init": (C.c_int, [_P, C.POINTER(C.c_ubyte), C.c_int, C.c_int]),
+    "td3_sync": (C.c_int, [_P]),
+    "td3_stream": (_P, [_P]),
+    "td3_profile_stages": (C.c_int, [_P, _P, C.c_int, C.c_int, _F, C.c_int, C.POINTER(C.c_int)]),
+    "td3_stage_name": (C.c_char_p, [_P, C.c_int]),
+    "td3_time_stage": (C.c_int, [_P, C.c_int, C.c_int, _F]),
+    "td3_stage_flops": (C.c_double, [_P, C.c_int]),
+    "td3_last_error": (C.c_char_p, []),
+}
+
+TD3_ACTOR, TD3_ACTOR_TARGET, TD3_CRITIC, TD3_CRITIC_TARGET = 0, 1, 2, 3
+TD3_ACTOR_ADAM_M, TD3_ACTOR_ADAM_V, TD3_CRITIC_ADAM_M, TD3_CRITIC_ADAM_V = 4, 5, 6, 7
+
+_lib = None
+_shutting_down = False
+
+
+def _mark_shutdown():
+    global _shutting_down
+    _shutting_down = True
+
+
+atexit.register(_mark_shutdown)
+
+
+def alive() -> bool:
+    """False once interpreter shutdown started (destructors must not call into HIP then)."""
+    return _lib is not None and not _shutting_down
+
+
+def load(path: str = LIB_PATH):
+    """Load libtd3hip.so and declare every exported signature (raises if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # torch bundles its own ROCm runtime (torch/lib/libamdhip64.so, soname
+    # libamdhip64.so.7).  Loading torch first makes our DT_NEEDED libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 / librccl.so.1 resolve to those already-loaded copies, so the
+    # process has ONE HIP runtime and torch streams / pointers are valid in our calls.
+    import torch  # noqa: F401
+    if not os.path.exists(path):
+        raise ImportError(
+            f"libtd3hip.so not found at {path}: build it with `python -m td3_amd.build` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class TD3Error(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = _lib.td3_last_error().decode(errors="replace") if _lib is not None else ""
+        raise TD3Error(f"{what} failed ({rc}): {msg}")
+
+
+def fptr(a):
+    """float* of a C-contiguous float32 numpy array."""
+    return a.ctypes.data_as(_F)
+
+
+def i64ptr(a):
+    return a.ctypes.data_as(_I64)
+
+
+def dptr(a):
+    return a.ctypes.data_as(_D)

@@ -1,0 +1,53 @@
+// HBM-resident replay ring (device side of my_replay_buffer.ReplayBuffer_*).
+#pragma once
+#include "common.h"
+
+namespace td3 {
+
+// One transition = one AoS record of `rec` floats in HBM:
+//   [ state(sd) | action(ad) | next_state(sd) | reward | not_done | pad to 16 B ]
+// (the reference keeps 5 float64 SoA arrays, my_replay_buffer.py:81-85; one
+// record per row makes the sample gather one contiguous read per index).
+struct Ring {
+  int sd = 0, ad = 0;
+  int rec = 0;
+  int o_s = 0, o_a = 0, o_s2 = 0, o_r = 0, o_nd = 0;
+  int64_t cap = 0;
+  int64_t ptr = 0, size = 0;       // host mirror of my_replay_buffer.py:76-77
+  float* data = nullptr;           // [cap][rec]
+  int64_t* d_size = nullptr;       // device copy of `size` (read by graph-replayed sample)
+  uint64_t seed = 0;
+  uint64_t sample_calls = 0;       // Philox counter of the stand-alone sample()
+  int device = 0;
+  hipStream_t stream = nullptr;
+  float* stage = nullptr;          // pinned host staging for add()
+  size_t stage_cap = 0;
+  hipEvent_t stage_ev = nullptr;
+  int64_t* d_idx = nullptr;        // last drawn indices (rows) of sample()
+  int idx_cap = 0;
+};
+
+// One gather destination: rows [0, Bp) of dst[r*ld + col + c] = record[src + c], c < len.
+struct GatherSeg {
+  float* dst;
+  int ld, col, src, len;
+};
+
+constexpr int kMaxSegs = 10;
+struct GatherArgs {
+  GatherSeg seg[kMaxSegs];
+  int nseg;
+  int B, Bp;
+  const float* data;
+  int rec;
+  const int64_t* d_size;        // sample range [0, *d_size)
+  const int64_t* inject_idx;    // nullable: use these rows instead of Philox
+  int64_t* idx_out;             // nullable: record drawn rows
+  uint64_t seed;
+  const Counters* ctr;          // nullable: Philox step = ctr->total_it + 1
+  uint64_t step;                // used when ctr == nullptr
+};
+
+int launch_gather(const GatherArgs& a, hipStream_t s);
+
+}  // namespace td3

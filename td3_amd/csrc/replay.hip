@@ -1,0 +1,327 @@
+// Replay ring kernels + the rb_* C-ABI (include/td3.h).
+//
+// Reference: /root/reference/my_replay_buffer.py
+//   ReplayBuffer_featured.__init__  :73-89   -> rb_create
+//   ReplayBuffer_featured.add       :109-117 -> rb_add (batched, pinned staging, async H2D)
+//   ReplayBuffer_featured.sample    :119-128 -> rb_sample / gather_kernel (Philox + HBM gather)
+//   ReplayBuffer_featured.save/load :91-107  -> rb_read_records / rb_write_records
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+
+#include "replay.h"
+#include "../../include/td3.h"
+
+namespace td3 {
+
+// ------------------------------------------------------------------ gather
+// One wave per sampled row: the row index is drawn once per wave, the record
+// (rec floats, 16-B aligned) is read as float4 and scattered into every
+// destination segment.  Rows B..Bp-1 are zero-filled so padded batch rows stay
+// finite and contribute nothing downstream.
+__global__ __launch_bounds__(256) void gather_kernel(GatherArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.Bp) return;
+  if (row >= a.B) {
+    for (int s = 0; s < a.nseg; ++s) {
+      const GatherSeg g = a.seg[s];
+      for (int c = lane; c < g.len; c += 64) g.dst[(size_t)row * g.ld + g.col + c] = 0.f;
+    }
+    return;
+  }
+  int64_t idx;
+  if (a.inject_idx) {
+    idx = a.inject_idx[row];
+  } else {
+    const uint64_t step = a.ctr ? (uint64_t)(a.ctr->total_it + 1) : a.step;
+    const int64_t n = *a.d_size;
+    idx = (int64_t)philox_index(a.seed, step, (uint32_t)row, (uint64_t)n);
+  }
+  if (a.idx_out && lane == 0) a.idx_out[row] = idx;
+  const float* src = a.data + (size_t)idx * a.rec;
+  for (int s = 0; s < a.nseg; ++s) {
+    const GatherSeg g = a.seg[s];
+    float* d = g.dst + (size_t)row * g.ld + g.col;
+    for (int c = lane; c < g.len; c += 64) d[c] = src[g.src + c];
+  }
+}
+
+int launch_gather(const GatherArgs& a, hipStream_t s) {
+  if (a.Bp <= 0) return 0;
+  dim3 grid((a.Bp + 3) / 4);
+  hipLaunchKernelGGL(gather_kernel, grid, dim3(256), 0, s, a);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ synthetic fill
+// state, next_state ~ N(0,1); action ~ U(-max_action, max_action);
+// reward ~ N(0,1); not_done = 1 with probability 0.99.  Philox keyed by (seed, row).
+__global__ __launch_bounds__(256) void fill_kernel(float* data, int rec, int sd, int ad,
+                                                   int64_t start, int64_t n, int64_t cap,
+                                                   float max_action, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t slot = (start + i) % cap;
+  float* r = data + (size_t)slot * rec;
+  const int nf = 2 * sd + ad + 2;
+  for (int c0 = lane * 4; c0 < rec; c0 += 256) {
+    float z[4];
+    philox_normal4(seed, (uint64_t)i, kStreamFill, (uint32_t)c0, z);
+    u32x4 u = philox4x32_10(u32x4{(uint32_t)c0, kStreamFill + 7u, (uint32_t)i, (uint32_t)(i >> 32)},
+                            (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + j;
+      if (c >= rec) break;
+      float v;
+      if (c >= nf) v = 0.f;
+      else if (c < sd) v = z[j];
+      else if (c < sd + ad) v = max_action * (2.f * ((float)(uu[j] >> 8) * (1.f / 16777216.f)) - 1.f);
+      else if (c < 2 * sd + ad) v = z[j];
+      else if (c == 2 * sd + ad) v = z[j];
+      else v = ((float)(uu[j] >> 8) * (1.f / 16777216.f)) < 0.01f ? 0.f : 1.f;
+      r[c] = v;
+    }
+  }
+}
+
+__global__ void set_i64_kernel(int64_t* p, int64_t v) { *p = v; }
+
+}  // namespace td3
+
+using namespace td3;
+
+// ================================================================== C-ABI
+extern "C" {
+
+int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint64_t seed,
+              rb_handle** out) {
+  TD3_ARG(out != nullptr, "out is null");
+  TD3_ARG(state_dim > 0 && action_dim > 0, "dims must be positive");
+  TD3_ARG(max_size > 0, "max_size must be positive");
+  TD3_HIP(hipSetDevice(device));
+  Ring* r = new Ring();
+  r->sd = state_dim;
+  r->ad = action_dim;
+  r->o_s = 0;
+  r->o_a = state_dim;
+  r->o_s2 = state_dim + action_dim;
+  r->o_r = 2 * state_dim + action_dim;
+  r->o_nd = r->o_r + 1;
+  r->rec = pad4(2 * state_dim + action_dim + 2);
+  r->cap = max_size;
+  r->seed = seed;
+  r->device = device;
+  hipError_t e = hipMalloc(&r->data, (size_t)max_size * r->rec * sizeof(float));
+  if (e != hipSuccess) {
+    set_error("rb_create: hipMalloc(%zu bytes) failed: %s",
+              (size_t)max_size * r->rec * sizeof(float), hipGetErrorString(e));
+    delete r;
+    return -2;
+  }
+  TD3_HIP(hipMemset(r->data, 0, (size_t)max_size * r->rec * sizeof(float)));
+  TD3_HIP(hipMalloc(&r->d_size, sizeof(int64_t)));
+  TD3_HIP(hipMemset(r->d_size, 0, sizeof(int64_t)));
+  TD3_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+  TD3_HIP(hipEventCreateWithFlags(&r->stage_ev, hipEventDisableTiming));
+  *out = reinterpret_cast<rb_handle*>(r);
+  return 0;
+}
+
+int rb_destroy(rb_handle* h) {
+  if (!h) return 0;
+  Ring* r = reinterpret_cast<Ring*>(h);
+  hipSetDevice(r->device);
+  hipStreamSynchronize(r->stream);
+  hipFree(r->data);
+  hipFree(r->d_size);
+  hipFree(r->d_idx);
+  if (r->stage) hipHostFree(r->stage);
+  hipEventDestroy(r->stage_ev);
+  hipStreamDestroy(r->stream);
+  delete r;
+  return 0;
+}
+
+int rb_info(const rb_handle* h, rb_info_t* info) {
+  TD3_ARG(h && info, "null handle");
+  const Ring* r = reinterpret_cast<const Ring*>(h);
+  info->state_dim = r->sd;
+  info->action_dim = r->ad;
+  info->record_floats = r->rec;
+  info->max_size = r->cap;
+  info->ptr = r->ptr;
+  info->size = r->size;
+  info->data = r->data;
+  info->device = r->device;
+  return 0;
+}
+
+static int ensure_stage(Ring* r, size_t floats) {
+  if (floats <= r->stage_cap) {
+    TD3_HIP(hipEventSynchronize(r->stage_ev));   // previous async H2D has consumed it
+    return 0;
+  }
+  TD3_HIP(hipEventSynchronize(r->stage_ev));
+  if (r->stage) TD3_HIP(hipHostFree(r->stage));
+  size_t cap = std::max(floats, (size_t)r->rec * 4096);
+  TD3_HIP(hipHostMalloc(&r->stage, cap * sizeof(float), hipHostMallocDefault));
+  r->stage_cap = cap;
+  return 0;
+}
+
+// Copy n packed records (host staging) into the ring at ptr, wrapping (the ring
+// semantics of my_replay_buffer.py:115-116 applied n times).
+static int push_staged(Ring* r, const float* host, int64_t n, hipStream_t stream) {
+  int64_t done = 0;
+  // Only the last `cap` records survive when n > cap.
+  if (n > r->cap) {
+    int64_t skip = n - r->cap;
+    r->ptr = (r->ptr + skip) % r->cap;
+    host += (size_t)skip * r->rec;
+    n = r->cap;
+    r->size = r->cap;
+  }
+  while (done < n) {
+    int64_t chunk = std::min<int64_t>(n - done, r->cap - r->ptr);
+    TD3_HIP(hipMemcpyAsync(r->data + (size_t)r->ptr * r->rec, host + (size_t)done * r->rec,
+                           (size_t)chunk * r->rec * sizeof(float), hipMemcpyHostToDevice, stream));
+    r->ptr = (r->ptr + chunk) % r->cap;
+    done += chunk;
+  }
+  r->size = std::min<int64_t>(r->size + n, r->cap);
+  hipLaunchKernelGGL(set_i64_kernel, dim3(1), dim3(1), 0, stream, r->d_size, r->size);
+  TD3_HIP(hipGetLastError());
+  TD3_HIP(hipEventRecord(r->stage_ev, stream));
+  return 0;
+}
+
+int rb_add(rb_handle* h, const double* state, const double* action, const double* next_state,
+           const double* reward, const double* done, int64_t n, void* stream) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(n >= 0, "n must be >= 0");
+  if (n == 0) return 0;
+  TD3_ARG(state && action && next_state && reward && done, "null input");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_HIP(hipSetDevice(r->device));
+  int rc = ensure_stage(r, (size_t)n * r->rec);
+  if (rc) return rc;
+  for (int64_t i = 0; i < n; ++i) {
+    float* d = r->stage + (size_t)i * r->rec;
+    for (int c = 0; c < r->sd; ++c) d[r->o_s + c] = (float)state[i * r->sd + c];
+    for (int c = 0; c < r->ad; ++c) d[r->o_a + c] = (float)action[i * r->ad + c];
+    for (int c = 0; c < r->sd; ++c) d[r->o_s2 + c] = (float)next_state[i * r->sd + c];
+    d[r->o_r] = (float)reward[i];
+    d[r->o_nd] = (float)(1.0 - done[i]);                  // my_replay_buffer.py:114
+    for (int c = r->o_nd + 1; c < r->rec; ++c) d[c] = 0.f;
+  }
+  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
+  return push_staged(r, r->stage, n, s);
+}
+
+int rb_add_records(rb_handle* h, const float* records, int64_t n, void* stream) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(n >= 0, "n must be >= 0");
+  if (n == 0) return 0;
+  TD3_ARG(records != nullptr, "null records");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_HIP(hipSetDevice(r->device));
+  int rc = ensure_stage(r, (size_t)n * r->rec);
+  if (rc) return rc;
+  memcpy(r->stage, records, (size_t)n * r->rec * sizeof(float));
+  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
+  return push_staged(r, r->stage, n, s);
+}
+
+int rb_fill_synthetic(rb_handle* h, int64_t n, float max_action, uint64_t seed, void* stream) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(n >= 0, "n must be >= 0");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_HIP(hipSetDevice(r->device));
+  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
+  if (n > r->cap) n = r->cap;
+  if (n > 0) {
+    dim3 grid((unsigned)((n + 3) / 4));
+    hipLaunchKernelGGL(fill_kernel, grid, dim3(256), 0, s, r->data, r->rec, r->sd, r->ad, r->ptr,
+                       n, r->cap, max_action, seed);
+    TD3_HIP(hipGetLastError());
+  }
+  r->ptr = (r->ptr + n) % r->cap;
+  r->size = std::min<int64_t>(r->size + n, r->cap);
+  hipLaunchKernelGGL(set_i64_kernel, dim3(1), dim3(1), 0, s, r->d_size, r->size);
+  TD3_HIP(hipGetLastError());
+  TD3_HIP(hipEventRecord(r->stage_ev, s));
+  return 0;
+}
+
+int rb_sample(rb_handle* h, int batch, float* state, float* action, float* next_state,
+              float* reward, float* not_done, const int64_t* inject_idx, int64_t* idx_out,
+              void* stream) {
+  TD3_ARG(h != nullptr, "null handle");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_ARG(batch >= 0, "batch must be >= 0");
+  TD3_ARG(r->size > 0 || batch == 0 || inject_idx, "sample from an empty buffer");
+  TD3_ARG(state && action && next_state && reward && not_done, "null output");
+  TD3_HIP(hipSetDevice(r->device));
+  GatherArgs a{};
+  a.seg[0] = GatherSeg{state, r->sd, 0, r->o_s, r->sd};
+  a.seg[1] = GatherSeg{action, r->ad, 0, r->o_a, r->ad};
+  a.seg[2] = GatherSeg{next_state, r->sd, 0, r->o_s2, r->sd};
+  a.seg[3] = GatherSeg{reward, 1, 0, r->o_r, 1};
+  a.seg[4] = GatherSeg{not_done, 1, 0, r->o_nd, 1};
+  a.nseg = 5;
+  a.B = a.Bp = batch;
+  a.data = r->data;
+  a.rec = r->rec;
+  a.d_size = r->d_size;
+  a.inject_idx = inject_idx;
+  a.idx_out = idx_out;
+  a.seed = r->seed;
+  a.ctr = nullptr;
+  a.step = ++r->sample_calls;
+  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
+  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));   // add() before sample() (main.py:261, :269)
+  return launch_gather(a, s);
+}
+
+int rb_read_records(const rb_handle* h, int64_t start, int64_t n, float* out) {
+  TD3_ARG(h && out, "null argument");
+  const Ring* r = reinterpret_cast<const Ring*>(h);
+  TD3_ARG(start >= 0 && n >= 0 && start + n <= r->cap, "range out of bounds");
+  TD3_HIP(hipSetDevice(r->device));
+  TD3_HIP(hipStreamSynchronize(r->stream));
+  TD3_HIP(hipDeviceSynchronize());
+  TD3_HIP(hipMemcpy(out, r->data + (size_t)start * r->rec, (size_t)n * r->rec * sizeof(float),
+                    hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int rb_write_records(rb_handle* h, int64_t start, int64_t n, const float* in, int64_t ptr,
+                     int64_t size) {
+  TD3_ARG(h && in, "null argument");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_ARG(start >= 0 && n >= 0 && start + n <= r->cap, "range out of bounds");
+  TD3_ARG(ptr >= 0 && ptr < r->cap && size >= 0 && size <= r->cap, "ptr/size out of bounds");
+  TD3_HIP(hipSetDevice(r->device));
+  TD3_HIP(hipDeviceSynchronize());
+  TD3_HIP(hipMemcpy(r->data + (size_t)start * r->rec, in, (size_t)n * r->rec * sizeof(float),
+                    hipMemcpyHostToDevice));
+  r->ptr = ptr;
+  r->size = size;
+  TD3_HIP(hipMemcpy(r->d_size, &r->size, sizeof(int64_t), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int rb_sync(rb_handle* h) {
+  TD3_ARG(h != nullptr, "null handle");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_HIP(hipSetDevice(r->device));
+  TD3_HIP(hipStreamSynchronize(r->stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1304 @@
+// Learner state, step planning, hipGraph replay and the td3_* C-ABI (include/td3.h).
+//
+// Reference mapping (/root/reference):
+//   TD3_featured.TD3.__init__   :100-110  -> td3_create (param arenas, targets = copies)
+//   TD3_featured.TD3.train      :123-171  -> td3_train_step (the stage list built by build_step)
+//   TD3_featured.TD3.select_action :113-115 -> td3_select_action
+//   TD3_featured.TD3.eval_q     :117-121  -> td3_eval_q
+//   TD3_base save/load          TD3_base.py:26-50 -> td3_get_params / td3_set_params
+//
+// HBM layout
+//   * one fp32 arena per parameter group (actor: 1 MLP; critic: q1 then q2), five
+//     parallel copies: params P, targets T, Adam exp_avg M, exp_avg_sq V, grads G.
+//     Every Linear weight is stored [pad32(out)][pad32(in)] (zero pads, which stay
+//     exactly zero through Adam and Polyak), biases / LayerNorm affines [pad32(out)].
+//   * one scratch arena for the batch: padded inputs, per-network activations
+//     H (post-ReLU), U (post-LN), LN row stats, and the backward dU / dZ rows.
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cmath>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "replay.h"
+#include "../../include/td3.h"
+
+namespace td3 {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+#define TD3_RC(expr)          \
+  do {                        \
+    int _rc = (expr);         \
+    if (_rc) return _rc;      \
+  } while (0)
+
+// ------------------------------------------------------------------ layouts
+struct LinearL { int N, K, Np, Kp; int64_t offW, offb; };
+struct LNormL { int N, Np; int64_t offg, offb; };
+struct NetL {
+  LinearL lin[4];
+  LNormL ln[3];
+};
+struct TensorRef { std::string name; int64_t rows, cols; int64_t off; int ld; };
+
+struct Group {
+  int64_t size = 0;          // floats per arena copy
+  float *P = nullptr, *T = nullptr, *M = nullptr, *V = nullptr, *G = nullptr;
+  std::vector<NetL> nets;
+  std::vector<TensorRef> tensors;
+};
+
+static NetL layout_mlp(int in, const int hid[3], int out, bool norm, const std::string& prefix,
+                       int64_t& off, std::vector<TensorRef>& tensors) {
+  NetL n{};
+  int dims[5] = {in, hid[0], hid[1], hid[2], out};
+  for (int l = 0; l < 4; ++l) {
+    LinearL& L = n.lin[l];
+    L.K = dims[l];
+    L.N = dims[l + 1];
+    L.Kp = pad32(L.K);
+    L.Np = pad32(L.N);
+    L.offW = off;
+    off += (int64_t)L.Np * L.Kp;
+    L.offb = off;
+    off += L.Np;
+    tensors.push_back({prefix + "linears." + std::to_string(l) + ".weight", L.N, L.K, L.offW, L.Kp});
+    tensors.push_back({prefix + "linears." + std::to_string(l) + ".bias", L.N, 0, L.offb, 0});
+  }
+  for (int l = 0; l < 3; ++l) {
+    LNormL& Ln = n.ln[l];
+    Ln.N = dims[l + 1];
+    Ln.Np = pad32(Ln.N);
+    Ln.offg = off;
+    off += Ln.Np;
+    Ln.offb = off;
+    off += Ln.Np;
+    if (norm) {
+      tensors.push_back({prefix + "lnorms." + std::to_string(l) + ".weight", Ln.N, 0, Ln.offg, 0});
+      tensors.push_back({prefix + "lnorms." + std::to_string(l) + ".bias", Ln.N, 0, Ln.offb, 0});
+    }
+  }
+  return n;
+}
+
+// ------------------------------------------------------------------ per-batch buffers
+struct EvalB {
+  float* X = nullptr; int ldx = 0;
+  float* H[3] = {};
+  float* U[3] = {};
+  float* stats[3] = {};
+  float* GU[3] = {};
+  float* GZ[4] = {};
+  float* T = nullptr;   // policy head tanh output [Bp][32]
+  float* Qv = nullptr;  // [Bp]
+};
+
+struct Scratch {
+  float* base = nullptr;
+  size_t cap = 0, used = 0;
+  float* take(size_t floats) {
+    size_t n = (floats + 63) & ~(size_t)63;
+    float* p = base + used;
+    used += n;
+    return p;
+  }
+};
+
+struct Stage {
+  std::string name;
+  std::function<int(hipStream_t)> run;
+  double flops = 0;
+};
+
+struct Plan {
+  int B = 0, Bp = 0;
+  float* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  // inputs
+  float *X_S = nullptr, *X_SA = nullptr, *X_S2 = nullptr, *X_S2A = nullptr, *X_SP = nullptr;
+  int ld_s = 0, ld_sa = 0;
+  float *R = nullptr, *ND = nullptr, *noise = nullptr, *Y = nullptr, *sqerr = nullptr;
+  int64_t* d_idx = nullptr;
+  int64_t* d_inject_idx = nullptr;
+  EvalB TA, Q[2], A, TQ[2], AQ;
+  // device problem tables (owned)
+  std::vector<void*> tables;
+  // stage lists (excluding the input stage): [actor_phase][inject_noise]
+  std::vector<Stage> body[2][2];
+  hipGraphExec_t graph[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+};
+
+struct ActPlan {       // select_action / eval_q at small batch
+  int Bp = 0;
+  float* scratch = nullptr;
+  float *X_S = nullptr, *X_SA = nullptr, *X_SP = nullptr;
+  EvalB A, Q[2];
+  std::vector<void*> tables;
+  std::vector<Stage> act, evalq;
+};
+
+}  // namespace td3
+
+using namespace td3;
+
+struct td3_handle {
+  td3_config cfg;
+  int sd, ad;
+  Group actor, critic;
+  float* arena = nullptr;
+  Counters* d_ctr = nullptr;
+  int64_t total_it = 0, critic_step = 0, actor_step = 0;   // host mirror
+  hipStream_t stream = nullptr;
+  std::unique_ptr<Plan> plan;
+  std::map<int, std::unique_ptr<ActPlan>> act;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  std::vector<Stage>* last_body = nullptr;
+  std::vector<std::string> stage_names;
+};
+
+namespace td3 {
+
+static int upload(td3_handle* h, std::vector<void*>& owned, const void* host, size_t bytes, void** out) {
+  void* d = nullptr;
+  TD3_HIP(hipMalloc(&d, bytes));
+  TD3_HIP(hipMemcpy(d, host, bytes, hipMemcpyHostToDevice));
+  owned.push_back(d);
+  *out = d;
+  (void)h;
+  return 0;
+}
+
+static void alloc_eval(Scratch& S, const NetL& n, int Bp, float* X, int ldx, bool bwd, bool norm,
+                       bool policy_or_q, EvalB& e) {
+  e.X = X;
+  e.ldx = ldx;
+  for (int l = 0; l < 3; ++l) {
+    const int Np = n.lin[l].Np;
+    e.H[l] = S.take((size_t)Bp * Np);
+    e.U[l] = norm ? S.take((size_t)Bp * Np) : e.H[l];
+    e.stats[l] = S.take((size_t)2 * Bp);
+    if (bwd) {
+      e.GU[l] = S.take((size_t)Bp * Np);
+      e.GZ[l] = S.take((size_t)Bp * Np);
+    }
+  }
+  if (bwd) e.GZ[3] = S.take((size_t)Bp * 32);
+  if (policy_or_q) {
+    e.T = S.take((size_t)Bp * 32);
+    e.Qv = S.take((size_t)Bp);
+  }
+}
+
+static int gemm_lds_bytes(int Kp) {
+  int f = std::max(32 * lds_stride(Kp), 4 * 32 * 33);
+  return f * 4;
+}
+
+// store_u: keep the LN outputs U (input of the dW of the next layer);
+// stats: keep the LN row statistics (needed by any backward through this network).
+struct FwdItem { const NetL* net; const float* P; EvalB* e; bool store_u; bool stats; };
+
+// Forward GEMM stages for layers 0..2 of several networks (one launch per layer).
+static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
+                          const std::vector<FwdItem>& items, int Bp, const char* tag,
+                          Counters* bump, int bump_actor) {
+  const bool norm = h->cfg.norm != 0;
+  for (int l = 0; l < 3; ++l) {
+    std::vector<GemmProb> probs;
+    int maxKp = 0;
+    for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Kp);
+    const int wn = maxKp <= 128 ? 4 : 1;
+    int blocks = 0;
+    double flops = 0;
+    int lds = 0;
+    for (auto& it : items) {
+      const LinearL& L = it.net->lin[l];
+      GemmProb p{};
+      if (l == 0) {
+        p.A = it.e->X;
+        p.lda = it.e->ldx;
+        p.pro = kProNone;
+      } else {
+        p.A = it.e->H[l - 1];
+        p.lda = it.net->lin[l - 1].Np;
+        if (norm) {
+          p.pro = kProLN;
+          p.lng = it.P + it.net->ln[l - 1].offg;
+          p.lnb = it.P + it.net->ln[l - 1].offb;
+          p.stats = it.stats ? it.e->stats[l - 1] : nullptr;
+          if (it.store_u) {
+            p.Aout = it.e->U[l - 1];
+            p.ldao = L.Kp;
+          }
+        } else {
+          p.pro = kProNone;
+        }
+      }
+      p.Kreal = L.K;
+      p.Kp = L.Kp;
+      p.W = it.P + L.offW;
+      p.ldw = L.Kp;
+      p.bias = it.P + L.offb;
+      p.Nout = L.Np;
+      p.C = it.e->H[l];
+      p.ldc = L.Np;
+      p.relu = 1;
+      p.ntiles = (L.Np + 32 * wn - 1) / (32 * wn);
+      p.tile_begin = blocks;
+      blocks += (Bp / 32) * p.ntiles;
+      flops += 2.0 * Bp * L.N * L.K;
+      lds = std::max(lds, gemm_lds_bytes(L.Kp));
+      probs.push_back(p);
+    }
+    void* d = nullptr;
+    TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
+    const int np = (int)probs.size();
+    Counters* bp = (l == 0) ? bump : nullptr;
+    const GemmProb* dp = (const GemmProb*)d;
+    st.push_back({std::string(tag) + "_fwd" + std::to_string(l),
+                  [=](hipStream_t s) { return launch_gemm(0, wn, dp, np, blocks, Bp, lds, bp, bump_actor, s); },
+                  flops});
+  }
+  return 0;
+}
+
+struct BwdItem { const NetL* net; const float* P; EvalB* e; };
+
+// dU_{l-1} = dZ_l * W_l for l = 2, 1 (dZ_1 formed in the prologue from dU_1), then dZ_0 rows.
+static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
+                          const std::vector<BwdItem>& items, int Bp, const char* tag, bool need_dz0) {
+  const bool norm = h->cfg.norm != 0;
+  for (int l = 2; l >= 1; --l) {
+    std::vector<GemmProb> probs;
+    int blocks = 0, lds = 0;
+    double flops = 0;
+    int maxKp = 0;
+    for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Np);
+    const int wn = maxKp <= 128 ? 4 : 1;
+    for (auto& it : items) {
+      const LinearL& L = it.net->lin[l];
+      GemmProb p{};
+      if (l == 2) {
+        p.A = it.e->GZ[2];
+        p.lda = L.Np;
+        p.pro = kProNone;
+      } else {
+        p.A = it.e->GU[1];
+        p.lda = L.Np;
+        p.pro = norm ? kProLNBwd : kProReluBwd;
+        p.H = it.e->H[1];
+        p.ldh = L.Np;
+        p.lng = it.P + it.net->ln[1].offg;
+        p.stats = it.e->stats[1];
+        p.Aout = it.e->GZ[1];
+        p.ldao = L.Np;
+      }
+      p.Kreal = L.N;
+      p.Kp = L.Np;
+      p.W = it.P + L.offW;
+      p.ldw = L.Kp;
+      p.Nout = L.Kp;
+      p.C = it.e->GU[l - 1];
+      p.ldc = L.Kp;
+      p.relu = 0;
+      p.ntiles = (L.Kp + 32 * wn - 1) / (32 * wn);
+      p.tile_begin = blocks;
+      blocks += (Bp / 32) * p.ntiles;
+      flops += 2.0 * Bp * L.N * L.K;
+      lds = std::max(lds, gemm_lds_bytes(L.Np));
+      probs.push_back(p);
+    }
+    void* d = nullptr;
+    TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
+    const int np = (int)probs.size();
+    const GemmProb* dp = (const GemmProb*)d;
+    st.push_back({std::string(tag) + "_bwd" + std::to_string(l),
+                  [=](hipStream_t s) { return launch_gemm(1, wn, dp, np, blocks, Bp, lds, nullptr, 0, s); },
+                  flops});
+  }
+  if (need_dz0) {
+    std::vector<LnBwdProb> probs;
+    for (auto& it : items) {
+      const LinearL& L = it.net->lin[0];
+      LnBwdProb p{};
+      p.GU = it.e->GU[0];
+      p.H = it.e->H[0];
+      p.stats = it.e->stats[0];
+      p.lng = it.P + it.net->ln[0].offg;
+      p.ld = L.Np;
+      p.K = L.N;
+      p.GZ = it.e->GZ[0];
+      probs.push_back(p);
+    }
+    void* d = nullptr;
+    TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(LnBwdProb), &d));
+    const int np = (int)probs.size();
+    const LnBwdProb* dp = (const LnBwdProb*)d;
+    const int nrm = norm ? 1 : 0;
+    st.push_back({std::string(tag) + "_lnbwd0",
+                  [=](hipStream_t s) { return launch_lnbwd_rows(dp, np, Bp, nrm, s); }, 0});
+  }
+  return 0;
+}
+
+// Weight / bias / LN grads of every layer of `items`, fused with the optimizer.
+static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
+                        Group& g, int which, const std::vector<BwdItem>& items, int Bp,
+                        const char* tag, bool polyak) {
+  const bool norm = h->cfg.norm != 0;
+  std::vector<DwProb> probs;
+  int blocks = 0;
+  double flops = 0;
+  for (auto& it : items) {
+    const NetL& n = *it.net;
+    for (int l = 0; l < 4; ++l) {
+      const LinearL& L = n.lin[l];
+      DwProb p{};
+      p.G = it.e->GZ[l];
+      p.ldg = (l == 3) ? 32 : L.Np;
+      p.U = (l == 0) ? it.e->X : it.e->U[l - 1];
+      p.ldu = (l == 0) ? it.e->ldx : n.lin[l - 1].Np;
+      p.Np = L.Np;
+      p.Kp = L.Kp;
+      p.offW = L.offW;
+      p.offb = L.offb;
+      if (norm && l < 3) {
+        p.offg = n.ln[l].offg;
+        p.offbeta = n.ln[l].offb;
+        p.GU = it.e->GU[l];
+        p.ldgu = L.Np;
+        p.H = it.e->H[l];
+        p.ldh = L.Np;
+        p.stats = it.e->stats[l];
+      } else {
+        p.offg = -1;
+        p.offbeta = -1;
+      }
+      p.ntk = L.Kp / 32;
+      p.tile_begin = blocks;
+      blocks += (L.Np / 32) * p.ntk;
+      flops += 2.0 * Bp * L.N * L.K;
+      probs.push_back(p);
+    }
+  }
+  void* d = nullptr;
+  TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(DwProb), &d));
+  DwArgs a{};
+  a.probs = (const DwProb*)d;
+  a.nprob = (int)probs.size();
+  a.Bp = Bp;
+  a.adam.P = g.P;
+  a.adam.G = g.G;
+  a.adam.M = g.M;
+  a.adam.V = g.V;
+  a.adam.T = g.T;
+  a.adam.ctr = h->d_ctr;
+  a.adam.which = which;
+  a.adam.lr = h->cfg.lr;
+  a.adam.beta1 = h->cfg.beta1;
+  a.adam.beta2 = h->cfg.beta2;
+  a.adam.eps = h->cfg.eps;
+  a.adam.tau = (float)h->cfg.tau;
+  a.adam.grad_scale = 1.0f;
+  const bool dp = h->comm != nullptr;
+  a.mode = dp ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
+  st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops});
+  if (dp) {
+    ncclComm_t comm = h->comm;
+    float* G = g.G;
+    const int64_t n = g.size;
+    st.push_back({std::string(tag) + "_allreduce",
+                  [=](hipStream_t s) {
+                    ncclResult_t r = ncclAllReduce(G, G, (size_t)n, ncclFloat, ncclSum, comm, s);
+                    if (r != ncclSuccess) {
+                      set_error("ncclAllReduce: %s", ncclGetErrorString(r));
+                      return -2;
+                    }
+                    return 0;
+                  },
+                  0});
+    AdamArgs aa = a.adam;
+    aa.grad_scale = 1.0f / (float)h->nranks;
+    const int pol = polyak ? 1 : 0;
+    st.push_back({std::string(tag) + "_adam",
+                  [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s); }, 0});
+  }
+  return 0;
+}
+
+static void free_plan_tables(std::vector<void*>& t) {
+  for (void* p : t) hipFree(p);
+  t.clear();
+}
+
+static void destroy_plan(Plan* p) {
+  if (!p) return;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      if (p->graph[a][b]) hipGraphExecDestroy(p->graph[a][b]);
+  free_plan_tables(p->tables);
+  if (p->scratch) hipFree(p->scratch);
+}
+
+static size_t eval_floats(const NetL& n, int Bp, bool bwd, bool norm) {
+  size_t f = 0;
+  for (int l = 0; l < 3; ++l) {
+    size_t np = (size_t)Bp * n.lin[l].Np;
+    f += np + 64;
+    if (norm) f += np + 64;
+    f += 2 * (size_t)Bp + 64;
+    if (bwd) f += 2 * (np + 64);
+  }
+  f += (size_t)Bp * 32 * 2 + Bp + 256;
+  return f;
+}
+
+static int build_step(td3_handle* h, int B) {
+  std::unique_ptr<Plan> P(new Plan());
+  const int Bp = pad32(B);
+  P->B = B;
+  P->Bp = Bp;
+  const bool norm = h->cfg.norm != 0;
+  const int sd = h->sd, ad = h->ad;
+  P->ld_s = pad32(sd);
+  P->ld_sa = pad32(sd + ad);
+  const NetL& an = h->actor.nets[0];
+  const NetL& q1 = h->critic.nets[0];
+  const NetL& q2 = h->critic.nets[1];
+  size_t floats = (size_t)Bp * (2 * P->ld_s + 3 * P->ld_sa) + 8 * (size_t)Bp + (size_t)Bp * ad + 4096;
+  floats += eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, true, norm) +
+            eval_floats(an, Bp, true, norm) + 2 * eval_floats(q1, Bp, false, norm) +
+            eval_floats(q1, Bp, true, norm) + 1024;
+  P->scratch_bytes = floats * sizeof(float);
+  TD3_HIP(hipMalloc(&P->scratch, P->scratch_bytes));
+  TD3_HIP(hipMemset(P->scratch, 0, P->scratch_bytes));
+  Scratch S{P->scratch, floats, 0};
+  P->X_S = S.take((size_t)Bp * P->ld_s);
+  P->X_S2 = S.take((size_t)Bp * P->ld_s);
+  P->X_SA = S.take((size_t)Bp * P->ld_sa);
+  P->X_S2A = S.take((size_t)Bp * P->ld_sa);
+  P->X_SP = S.take((size_t)Bp * P->ld_sa);
+  P->R = S.take(Bp);
+  P->ND = S.take(Bp);
+  P->noise = S.take((size_t)Bp * ad);
+  P->Y = S.take(Bp);
+  P->sqerr = S.take(2 * (size_t)Bp);
+  P->d_idx = (int64_t*)S.take(2 * (size_t)Bp);
+  P->d_inject_idx = (int64_t*)S.take(2 * (size_t)Bp);
+  alloc_eval(S, an, Bp, P->X_S2, P->ld_s, false, norm, false, P->TA);
+  alloc_eval(S, q1, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[0]);
+  alloc_eval(S, q2, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[1]);
+  alloc_eval(S, an, Bp, P->X_S, P->ld_s, true, norm, true, P->A);
+  alloc_eval(S, q1, Bp, P->X_S2A, P->ld_sa, false, norm, true, P->TQ[0]);
+  alloc_eval(S, q2, Bp, P->X_S2A, P->ld_sa, false, norm, true, P->TQ[1]);
+  alloc_eval(S, q1, Bp, P->X_SP, P->ld_sa, true, norm, true, P->AQ);
+  if (S.used > S.cap) {
+    set_error("internal: scratch overflow (%zu > %zu)", S.used, S.cap);
+    return -2;
+  }
+
+  // Layout offsets are absolute inside each group arena, so every network of a group
+  // uses the group's base pointer (q1 and q2 simply have different offsets).
+  const float* Pa = h->actor.P;
+  const float* Pta = h->actor.T;
+  const float* Pq1 = h->critic.P;
+  const float* Pq2 = h->critic.P;
+  const float* Ptq1 = h->critic.T;
+  const float* Ptq2 = h->critic.T;
+
+  for (int actor_phase = 0; actor_phase < 2; ++actor_phase) {
+    for (int inj = 0; inj < 2; ++inj) {
+      std::vector<Stage>& st = P->body[actor_phase][inj];
+      // ---- forward of target actor, online twin (and online actor on policy steps)
+      std::vector<FwdItem> f1 = {{&an, Pta, &P->TA, false, false}, {&q1, Pq1, &P->Q[0], true, true},
+                                 {&q2, Pq2, &P->Q[1], true, true}};
+      if (actor_phase) f1.push_back({&an, Pa, &P->A, true, true});
+      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, "F", h->d_ctr, actor_phase));
+      // ---- heads: next_action (target smoothing), Q1/Q2 values, pi(s)
+      {
+        std::vector<HeadProb> hp;
+        HeadProb p{};
+        auto base = [&](const NetL& n, const float* Pp, EvalB& e, int mode) {
+          HeadProb q{};
+          q.H3 = e.H[2];
+          q.ldh = n.lin[2].Np;
+          q.K3 = n.lin[2].N;
+          q.lng = norm ? Pp + n.ln[2].offg : nullptr;
+          q.lnb = norm ? Pp + n.ln[2].offb : nullptr;
+          q.W4 = Pp + n.lin[3].offW;
+          q.ldw = n.lin[3].Kp;
+          q.b4 = Pp + n.lin[3].offb;
+          q.nout = n.lin[3].N;
+          q.mode = mode;
+          return q;
+        };
+        p = base(an, Pta, P->TA, kHeadTargetAction);
+        p.out = P->X_S2A;
+        p.ldo = P->ld_sa;
+        p.out_col = sd;
+        p.noise = P->noise;
+        p.ldn = ad;
+        hp.push_back(p);
+        for (int j = 0; j < 2; ++j) {
+          const NetL& qn = j ? q2 : q1;
+          p = base(qn, j ? Pq2 : Pq1, P->Q[j], kHeadQ);
+          p.U3 = norm ? P->Q[j].U[2] : nullptr;
+          p.ldu = qn.lin[2].Np;
+          p.stats = P->Q[j].stats[2];
+          p.out = P->Q[j].Qv;
+          hp.push_back(p);
+        }
+        if (actor_phase) {
+          p = base(an, Pa, P->A, kHeadPolicy);
+          p.U3 = norm ? P->A.U[2] : nullptr;
+          p.ldu = an.lin[2].Np;
+          p.stats = P->A.stats[2];
+          p.out = P->X_SP;
+          p.ldo = P->ld_sa;
+          p.out_col = sd;
+          p.tanh_out = P->A.T;
+          hp.push_back(p);
+        }
+        void* d = nullptr;
+        TD3_RC(upload(h, P->tables, hp.data(), hp.size() * sizeof(HeadProb), &d));
+        HeadArgs a{};
+        a.probs = (const HeadProb*)d;
+        a.B = B;
+        a.Bp = Bp;
+        a.max_action = h->cfg.max_action;
+        a.policy_noise = (float)h->cfg.policy_noise;
+        a.noise_clip = (float)h->cfg.noise_clip;
+        a.ctr = h->d_ctr;
+        a.seed = h->cfg.seed;
+        a.gen_noise = inj ? 0 : 1;
+        const int np = (int)hp.size();
+        st.push_back({"heads", [=](hipStream_t s) { return launch_heads(a, np, s); }, 0});
+      }
+      // ---- target twin on (s', a')
+      std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
+      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, "TF", nullptr, 0));
+      // ---- critic loss + LN3 backward of the twin
+      {
+        CriticLossArgs a{};
+        for (int j = 0; j < 2; ++j) {
+          const NetL& qn = j ? q2 : q1;
+          const float* Pt = j ? Ptq2 : Ptq1;
+          const float* Pp = j ? Pq2 : Pq1;
+          a.TH3[j] = P->TQ[j].H[2];
+          a.Tlng[j] = Pt + qn.ln[2].offg;
+          a.Tlnb[j] = Pt + qn.ln[2].offb;
+          a.TW4[j] = Pt + qn.lin[3].offW;
+          a.Tb4[j] = Pt + qn.lin[3].offb;
+          a.Qv[j] = P->Q[j].Qv;
+          a.H3[j] = P->Q[j].H[2];
+          a.stats3[j] = P->Q[j].stats[2];
+          a.lng3[j] = Pp + qn.ln[2].offg;
+          a.W4[j] = Pp + qn.lin[3].offW;
+          a.GZ4[j] = P->Q[j].GZ[3];
+          a.GU3[j] = P->Q[j].GU[2];
+          a.GZ3[j] = P->Q[j].GZ[2];
+        }
+        a.ldgz4 = 32;
+        a.ldh = q1.lin[2].Np;
+        a.K3 = q1.lin[2].N;
+        a.R = P->R;
+        a.ND = P->ND;
+        a.Y = P->Y;
+        a.sqerr = P->sqerr;
+        a.B = B;
+        a.Bp = Bp;
+        a.discount = (float)h->cfg.discount;
+        a.norm = norm ? 1 : 0;
+        st.push_back({"critic_loss", [=](hipStream_t s) { return launch_critic_loss(a, s); }, 0});
+      }
+      std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0]}, {&q2, Pq2, &P->Q[1]}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, "CB", true));
+      TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0));
+      if (!actor_phase) continue;
+      // ---------------- delayed policy update (TD3_featured.py:156-171)
+      std::vector<FwdItem> f3 = {{&q1, Pq1, &P->AQ, false, true}};
+      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, "AF", nullptr, 0));
+      {
+        ActorLossArgs a{};
+        a.H3 = P->AQ.H[2];
+        a.ldh = q1.lin[2].Np;
+        a.K3 = q1.lin[2].N;
+        a.lng = Pq1 + q1.ln[2].offg;
+        a.lnb = Pq1 + q1.ln[2].offb;
+        a.W4 = Pq1 + q1.lin[3].offW;
+        a.b4 = Pq1 + q1.lin[3].offb;
+        a.Qv = P->AQ.Qv;
+        a.GZ3 = P->AQ.GZ[2];
+        a.B = B;
+        a.Bp = Bp;
+        a.norm = norm ? 1 : 0;
+        st.push_back({"actor_loss", [=](hipStream_t s) { return launch_actor_loss(a, s); }, 0});
+      }
+      std::vector<BwdItem> ab = {{&q1, Pq1, &P->AQ}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, "AQB", false));
+      {
+        ActorHeadBwdArgs a{};
+        a.GU1 = P->AQ.GU[0];
+        a.H1 = P->AQ.H[0];
+        a.stats1 = P->AQ.stats[0];
+        a.lng1 = Pq1 + q1.ln[0].offg;
+        a.ld1 = q1.lin[0].Np;
+        a.K1 = q1.lin[0].N;
+        a.W1 = Pq1 + q1.lin[0].offW;
+        a.ldw1 = q1.lin[0].Kp;
+        a.sd = sd;
+        a.ad = ad;
+        a.T = P->A.T;
+        a.ldt = 32;
+        a.max_action = h->cfg.max_action;
+        a.GZ4 = P->A.GZ[3];
+        a.ldgz4 = 32;
+        a.W4 = Pa + an.lin[3].offW;
+        a.ldw4 = an.lin[3].Kp;
+        a.H3 = P->A.H[2];
+        a.stats3 = P->A.stats[2];
+        a.lng3 = Pa + an.ln[2].offg;
+        a.ld3 = an.lin[2].Np;
+        a.K3 = an.lin[2].N;
+        a.GU3 = P->A.GU[2];
+        a.GZ3 = P->A.GZ[2];
+        a.B = B;
+        a.Bp = Bp;
+        a.norm = norm ? 1 : 0;
+        st.push_back({"actor_head_bwd", [=](hipStream_t s) { return launch_actor_head_bwd(a, s); }, 0});
+      }
+      std::vector<BwdItem> aa = {{&an, Pa, &P->A}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, aa, Bp, "AB", true));
+      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, aa, Bp, "A", true));
+    }
+  }
+  if (h->plan) destroy_plan(h->plan.get());
+  h->plan = std::move(P);
+  return 0;
+}
+
+static int run_stages(std::vector<Stage>& st, hipStream_t s) {
+  for (auto& x : st) TD3_RC(x.run(s));
+  return 0;
+}
+
+// Input stage: Philox index draw + gather from the ring into the padded batch buffers.
+static int input_from_ring(td3_handle* h, Ring* r, Plan* P, bool inject_idx, hipStream_t s) {
+  GatherArgs a{};
+  const int sd = h->sd, ad = h->ad;
+  int k = 0;
+  a.seg[k++] = GatherSeg{P->X_S, P->ld_s, 0, r->o_s, sd};
+  a.seg[k++] = GatherSeg{P->X_SA, P->ld_sa, 0, r->o_s, sd};
+  a.seg[k++] = GatherSeg{P->X_SA, P->ld_sa, sd, r->o_a, ad};
+  a.seg[k++] = GatherSeg{P->X_SP, P->ld_sa, 0, r->o_s, sd};
+  a.seg[k++] = GatherSeg{P->X_S2, P->ld_s, 0, r->o_s2, sd};
+  a.seg[k++] = GatherSeg{P->X_S2A, P->ld_sa, 0, r->o_s2, sd};
+  a.seg[k++] = GatherSeg{P->R, 1, 0, r->o_r, 1};
+  a.seg[k++] = GatherSeg{P->ND, 1, 0, r->o_nd, 1};
+  a.nseg = k;
+  a.B = P->B;
+  a.Bp = P->Bp;
+  a.data = r->data;
+  a.rec = r->rec;
+  a.d_size = r->d_size;
+  a.inject_idx = inject_idx ? P->d_inject_idx : nullptr;
+  a.idx_out = P->d_idx;
+  a.seed = r->seed;
+  a.ctr = h->d_ctr;
+  return launch_gather(a, s);
+}
+
+__global__ void pack_kernel(const float* __restrict__ src, int cols, int B, int Bp, float* d1, int ld1,
+                            int c1, float* d2, int ld2, int c2, float* d3, int ld3, int c3) {
+  const int row = blockIdx.x;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    const float v = row < B ? src[(size_t)row * cols + c] : 0.f;
+    if (d1) d1[(size_t)row * ld1 + c1 + c] = v;
+    if (d2) d2[(size_t)row * ld2 + c2 + c] = v;
+    if (d3) d3[(size_t)row * ld3 + c3 + c] = v;
+  }
+  (void)Bp;
+}
+
+static int input_from_batch(td3_handle* h, Plan* P, const float* s, const float* a, const float* s2,
+                            const float* r, const float* nd, hipStream_t st) {
+  const int sd = h->sd, ad = h->ad, Bp = P->Bp, B = P->B;
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, s, sd, B, Bp, P->X_S, P->ld_s, 0,
+                     P->X_SA, P->ld_sa, 0, P->X_SP, P->ld_sa, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, a, ad, B, Bp, P->X_SA, P->ld_sa, sd,
+                     (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, s2, sd, B, Bp, P->X_S2, P->ld_s, 0,
+                     P->X_S2A, P->ld_sa, 0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, r, 1, B, Bp, P->R, 1, 0,
+                     (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, nd, 1, B, Bp, P->ND, 1, 0,
+                     (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s) {
+  Plan* P = h->plan.get();
+  std::vector<Stage>& st = P->body[actor_phase][inj];
+  h->last_body = &st;
+  if (!h->cfg.use_graph) return run_stages(st, s);
+  hipGraphExec_t& ge = P->graph[actor_phase][inj];
+  if (!ge) {
+    hipStream_t cs;
+    TD3_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    TD3_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    int rc = run_stages(st, cs);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(cs, &g);
+    if (rc) {
+      if (g) hipGraphDestroy(g);
+      hipStreamDestroy(cs);
+      return rc;
+    }
+    TD3_HIP(e);
+    TD3_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    TD3_HIP(hipGraphDestroy(g));
+    TD3_HIP(hipStreamDestroy(cs));
+  }
+  TD3_HIP(hipGraphLaunch(ge, s));
+  return 0;
+}
+
+static int ensure_plan(td3_handle* h, int B) {
+  if (h->plan && h->plan->B == B) return 0;
+  TD3_HIP(hipStreamSynchronize(h->stream));
+  return build_step(h, B);
+}
+
+static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_stats* stats) {
+  h->total_it += 1;
+  h->critic_step += 1;
+  if (actor_phase) h->actor_step += 1;
+  if (!stats) return 0;
+  Plan* P = h->plan.get();
+  TD3_HIP(hipStreamSynchronize(s));
+  const int B = P->B, Bp = P->Bp;
+  std::vector<float> sq(2 * (size_t)Bp);
+  TD3_HIP(hipMemcpy(sq.data(), P->sqerr, sq.size() * 4, hipMemcpyDeviceToHost));
+  double l1 = 0, l2 = 0;
+  for (int i = 0; i < B; ++i) {
+    l1 += sq[i];
+    l2 += sq[Bp + i];
+  }
+  stats->critic_loss = l1 / B + l2 / B;
+  stats->actor_step = actor_phase;
+  stats->actor_loss = NAN;
+  if (actor_phase) {
+    std::vector<float> q(Bp);
+    TD3_HIP(hipMemcpy(q.data(), P->AQ.Qv, Bp * 4, hipMemcpyDeviceToHost));
+    double m = 0;
+    for (int i = 0; i < B; ++i) m += q[i];
+    stats->actor_loss = -m / B;
+  }
+  if (stats->y) TD3_HIP(hipMemcpy(stats->y, P->Y, B * 4, hipMemcpyDeviceToHost));
+  if (stats->q1) TD3_HIP(hipMemcpy(stats->q1, P->Q[0].Qv, B * 4, hipMemcpyDeviceToHost));
+  if (stats->q2) TD3_HIP(hipMemcpy(stats->q2, P->Q[1].Qv, B * 4, hipMemcpyDeviceToHost));
+  if (stats->idx) TD3_HIP(hipMemcpy(stats->idx, P->d_idx, B * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ------------------------------------------------------------------ act / eval_q plans
+static int build_act(td3_handle* h, int Bp, ActPlan** out) {
+  auto it = h->act.find(Bp);
+  if (it != h->act.end()) {
+    *out = it->second.get();
+    return 0;
+  }
+  std::unique_ptr<ActPlan> A(new ActPlan());
+  A->Bp = Bp;
+  const bool norm = h->cfg.norm != 0;
+  const NetL& an = h->actor.nets[0];
+  const NetL& q1 = h->critic.nets[0];
+  const NetL& q2 = h->critic.nets[1];
+  const int lds_s = pad32(h->sd), lds_sa = pad32(h->sd + h->ad);
+  size_t floats = (size_t)Bp * (lds_s + 2 * lds_sa) + eval_floats(an, Bp, false, norm) +
+                  2 * eval_floats(q1, Bp, false, norm) + 4096;
+  TD3_HIP(hipMalloc(&A->scratch, floats * 4));
+  TD3_HIP(hipMemset(A->scratch, 0, floats * 4));
+  Scratch S{A->scratch, floats, 0};
+  A->X_S = S.take((size_t)Bp * lds_s);
+  A->X_SA = S.take((size_t)Bp * lds_sa);
+  A->X_SP = S.take((size_t)Bp * lds_sa);
+  alloc_eval(S, an, Bp, A->X_S, lds_s, false, norm, true, A->A);
+  alloc_eval(S, q1, Bp, A->X_SA, lds_sa, false, norm, true, A->Q[0]);
+  alloc_eval(S, q2, Bp, A->X_SA, lds_sa, false, norm, true, A->Q[1]);
+  auto head = [&](const NetL& n, const float* Pp, EvalB& e, int mode) {
+    HeadProb q{};
+    q.H3 = e.H[2];
+    q.ldh = n.lin[2].Np;
+    q.K3 = n.lin[2].N;
+    q.lng = norm ? Pp + n.ln[2].offg : nullptr;
+    q.lnb = norm ? Pp + n.ln[2].offb : nullptr;
+    q.W4 = Pp + n.lin[3].offW;
+    q.ldw = n.lin[3].Kp;
+    q.b4 = Pp + n.lin[3].offb;
+    q.nout = n.lin[3].N;
+    q.mode = mode;
+    return q;
+  };
+  {
+    std::vector<FwdItem> f = {{&an, h->actor.P, &A->A, false, false}};
+    TD3_RC(add_fwd_stages(h, A->tables, A->act, f, Bp, "act", nullptr, 0));
+    HeadProb p = head(an, h->actor.P, A->A, kHeadPolicy);
+    p.out = A->X_SP;
+    p.ldo = lds_sa;
+    p.out_col = h->sd;
+    p.tanh_out = A->A.T;
+    void* d = nullptr;
+    TD3_RC(upload(h, A->tables, &p, sizeof(p), &d));
+    HeadArgs a{};
+    a.probs = (const HeadProb*)d;
+    a.B = Bp;
+    a.Bp = Bp;
+    a.max_action = h->cfg.max_action;
+    A->act.push_back({"act_head", [=](hipStream_t s) { return launch_heads(a, 1, s); }, 0});
+  }
+  {
+    std::vector<FwdItem> f = {{&q1, h->critic.P, &A->Q[0], false, false},
+                              {&q2, h->critic.P, &A->Q[1], false, false}};
+    TD3_RC(add_fwd_stages(h, A->tables, A->evalq, f, Bp, "evq", nullptr, 0));
+    std::vector<HeadProb> hp;
+    for (int j = 0; j < 2; ++j) {
+      HeadProb p = head(j ? q2 : q1, h->critic.P, A->Q[j], kHeadQ);
+      p.out = A->Q[j].Qv;
+      hp.push_back(p);
+    }
+    void* d = nullptr;
+    TD3_RC(upload(h, A->tables, hp.data(), hp.size() * sizeof(HeadProb), &d));
+    HeadArgs a{};
+    a.probs = (const HeadProb*)d;
+    a.B = Bp;
+    a.Bp = Bp;
+    a.max_action = h->cfg.max_action;
+    A->evalq.push_back({"evq_head", [=](hipStream_t s) { return launch_heads(a, 2, s); }, 0});
+  }
+  *out = A.get();
+  h->act[Bp] = std::move(A);
+  return 0;
+}
+
+static int copy_rows_h2d(float* dst, int ld, int col, const float* src, int n, int cols, hipStream_t s) {
+  TD3_HIP(hipMemcpy2DAsync(dst + col, (size_t)ld * 4, src, (size_t)cols * 4, (size_t)cols * 4, n,
+                           hipMemcpyHostToDevice, s));
+  return 0;
+}
+
+}  // namespace td3
+
+// ================================================================== C-ABI
+extern "C" {
+
+const char* td3_last_error(void) { return g_err; }
+
+void td3_default_config(td3_config* c) {
+  memset(c, 0, sizeof(*c));
+  c->actor_hidden[0] = 500; c->actor_hidden[1] = 400; c->actor_hidden[2] = 300;    // TD3_featured.py:19
+  c->critic_hidden[0] = 500; c->critic_hidden[1] = 400; c->critic_hidden[2] = 200; // TD3_featured.py:54
+  c->norm = 1;
+  c->max_action = 1.0f;
+  c->discount = 0.99;       // TD3_base.py:9 / main.py:112
+  c->tau = 0.005;
+  c->policy_noise = 0.2;
+  c->noise_clip = 0.5;
+  c->policy_freq = 2;
+  c->lr = 1e-4;             // TD3_featured.py:100 / main.py:116
+  c->beta1 = 0.9;
+  c->beta2 = 0.999;
+  c->eps = 1e-8;
+  c->seed = 0;
+  c->device = 0;
+  c->use_graph = 1;
+}
+
+int td3_create(const td3_config* cfg, td3_handle** out) {
+  TD3_ARG(cfg && out, "null argument");
+  TD3_ARG(cfg->state_dim > 0 && cfg->action_dim > 0, "dims must be positive");
+  TD3_ARG(cfg->action_dim <= 32, "action_dim > 32 not supported by the head kernels");
+  TD3_ARG(cfg->policy_freq > 0, "policy_freq must be positive");
+  TD3_ARG(pad32(cfg->state_dim + cfg->action_dim) <= 512, "state_dim + action_dim must be <= 512");
+  for (int i = 0; i < 3; ++i) {
+    TD3_ARG(cfg->actor_hidden[i] > 0 && cfg->actor_hidden[i] <= 512, "actor hidden in (0, 512]");
+    TD3_ARG(cfg->critic_hidden[i] > 0 && cfg->critic_hidden[i] <= 512, "critic hidden in (0, 512]");
+  }
+  TD3_HIP(hipSetDevice(cfg->device));
+  TD3_RC(kernels_init());
+  td3_handle* h = new td3_handle();
+  h->cfg = *cfg;
+  h->sd = cfg->state_dim;
+  h->ad = cfg->action_dim;
+  const bool norm = cfg->norm != 0;
+  int64_t off = 0;
+  h->actor.nets.push_back(layout_mlp(h->sd, cfg->actor_hidden, h->ad, norm, "", off, h->actor.tensors));
+  h->actor.size = off;
+  off = 0;
+  h->critic.nets.push_back(layout_mlp(h->sd + h->ad, cfg->critic_hidden, 1, norm, "q1.", off, h->critic.tensors));
+  h->critic.nets.push_back(layout_mlp(h->sd + h->ad, cfg->critic_hidden, 1, norm, "q2.", off, h->critic.tensors));
+  h->critic.size = off;
+  const size_t total = 5 * (size_t)(h->actor.size + h->critic.size);
+  hipError_t e = hipMalloc(&h->arena, total * sizeof(float));
+  if (e != hipSuccess) {
+    set_error("td3_create: hipMalloc failed: %s", hipGetErrorString(e));
+    delete h;
+    return -2;
+  }
+  TD3_HIP(hipMemset(h->arena, 0, total * sizeof(float)));
+  float* p = h->arena;
+  for (Group* g : {&h->actor, &h->critic}) {
+    g->P = p; p += g->size;
+    g->T = p; p += g->size;
+    g->M = p; p += g->size;
+    g->V = p; p += g->size;
+    g->G = p; p += g->size;
+  }
+  TD3_HIP(hipMalloc(&h->d_ctr, sizeof(Counters)));
+  TD3_HIP(hipMemset(h->d_ctr, 0, sizeof(Counters)));
+  TD3_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  *out = h;
+  return 0;
+}
+
+int td3_destroy(td3_handle* h) {
+  if (!h) return 0;
+  hipSetDevice(h->cfg.device);
+  hipStreamSynchronize(h->stream);
+  if (h->plan) destroy_plan(h->plan.get());
+  for (auto& kv : h->act) {
+    free_plan_tables(kv.second->tables);
+    hipFree(kv.second->scratch);
+  }
+  if (h->comm) ncclCommDestroy(h->comm);
+  hipFree(h->arena);
+  hipFree(h->d_ctr);
+  hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+int td3_tensor_count(const td3_handle* h, int g) {
+  if (!h) return -1;
+  return (int)(g ? h->critic.tensors.size() : h->actor.tensors.size());
+}
+
+int td3_tensor_info(const td3_handle* h, int g, int i, char* name, int name_len, int64_t* rows,
+                    int64_t* cols) {
+  TD3_ARG(h != nullptr, "null handle");
+  const Group& G = g ? h->critic : h->actor;
+  TD3_ARG(i >= 0 && i < (int)G.tensors.size(), "tensor index out of range");
+  const TensorRef& t = G.tensors[i];
+  if (name && name_len > 0) snprintf(name, name_len, "%s", t.name.c_str());
+  if (rows) *rows = t.rows;
+  if (cols) *cols = t.cols;
+  return 0;
+}
+
+int64_t td3_num_params(const td3_handle* h, int g) {
+  if (!h) return -1;
+  const Group& G = g ? h->critic : h->actor;
+  int64_t n = 0;
+  for (auto& t : G.tensors) n += t.rows * (t.cols ? t.cols : 1);
+  return n;
+}
+
+static int which_ptr(td3_handle* h, int which, Group** g, float** base) {
+  switch (which) {
+    case TD3_ACTOR: *g = &h->actor; *base = h->actor.P; return 0;
+    case TD3_ACTOR_TARGET: *g = &h->actor; *base = h->actor.T; return 0;
+    case TD3_CRITIC: *g = &h->critic; *base = h->critic.P; return 0;
+    case TD3_CRITIC_TARGET: *g = &h->critic; *base = h->critic.T; return 0;
+    case TD3_ACTOR_ADAM_M: *g = &h->actor; *base = h->actor.M; return 0;
+    case TD3_ACTOR_ADAM_V: *g = &h->actor; *base = h->actor.V; return 0;
+    case TD3_CRITIC_ADAM_M: *g = &h->critic; *base = h->critic.M; return 0;
+    case TD3_CRITIC_ADAM_V: *g = &h->critic; *base = h->critic.V; return 0;
+  }
+  set_error("unknown tensor group %d", which);
+  return -1;
+}
+
+int td3_get_params(td3_handle* h, int which, float* out, int64_t n) {
+  TD3_ARG(h && out, "null argument");
+  Group* g;
+  float* base;
+  TD3_RC(which_ptr(h, which, &g, &base));
+  TD3_ARG(n == td3_num_params(h, g == &h->critic), "size mismatch");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_HIP(hipStreamSynchronize(h->stream));
+  TD3_HIP(hipDeviceSynchronize());
+  std::vector<float> host(g->size);
+  TD3_HIP(hipMemcpy(host.data(), base, g->size * 4, hipMemcpyDeviceToHost));
+  int64_t o = 0;
+  for (auto& t : g->tensors) {
+    if (t.cols) {
+      for (int64_t r = 0; r < t.rows; ++r)
+        memcpy(out + o + r * t.cols, host.data() + t.off + r * t.ld, t.cols * 4);
+      o += t.rows * t.cols;
+    } else {
+      memcpy(out + o, host.data() + t.off, t.rows * 4);
+      o += t.rows;
+    }
+  }
+  return 0;
+}
+
+int td3_set_params(td3_handle* h, int which, const float* in, int64_t n) {
+  TD3_ARG(h && in, "null argument");
+  Group* g;
+  float* base;
+  TD3_RC(which_ptr(h, which, &g, &base));
+  TD3_ARG(n == td3_num_params(h, g == &h->critic), "size mismatch");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_HIP(hipStreamSynchronize(h->stream));
+  TD3_HIP(hipDeviceSynchronize());
+  std::vector<float> host(g->size, 0.f);
+  int64_t o = 0;
+  for (auto& t : g->tensors) {
+    if (t.cols) {
+      for (int64_t r = 0; r < t.rows; ++r)
+        memcpy(host.data() + t.off + r * t.ld, in + o + r * t.cols, t.cols * 4);
+      o += t.rows * t.cols;
+    } else {
+      memcpy(host.data() + t.off, in + o, t.rows * 4);
+      o += t.rows;
+    }
+  }
+  TD3_HIP(hipMemcpy(base, host.data(), g->size * 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int td3_get_counters(const td3_handle* h, int64_t* total_it, int64_t* critic_step, int64_t* actor_step) {
+  TD3_ARG(h != nullptr, "null handle");
+  if (total_it) *total_it = h->total_it;
+  if (critic_step) *critic_step = h->critic_step;
+  if (actor_step) *actor_step = h->actor_step;
+  return 0;
+}
+
+int td3_set_counters(td3_handle* h, int64_t total_it, int64_t critic_step, int64_t actor_step) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(total_it >= 0 && critic_step >= 0 && actor_step >= 0, "negative counter");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_HIP(hipStreamSynchronize(h->stream));
+  Counters c{total_it, critic_step, actor_step, 0};
+  TD3_HIP(hipMemcpy(h->d_ctr, &c, sizeof(c), hipMemcpyHostToDevice));
+  h->total_it = total_it;
+  h->critic_step = critic_step;
+  h->actor_step = actor_step;
+  return 0;
+}
+
+int td3_train_step(td3_handle* h, rb_handle* rbh, int batch, void* stream, const int64_t* inject_idx,
+                   const float* inject_noise, td3_step_stats* stats) {
+  TD3_ARG(h && rbh, "null handle");
+  TD3_ARG(batch > 0, "batch must be positive");
+  Ring* r = reinterpret_cast<Ring*>(rbh);
+  TD3_ARG(r->sd == h->sd && r->ad == h->ad, "replay buffer dims do not match the learner");
+  TD3_ARG(r->size > 0 || inject_idx, "train on an empty replay buffer");
+  TD3_ARG(r->device == h->cfg.device, "replay buffer lives on another device");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_RC(ensure_plan(h, batch));
+  Plan* P = h->plan.get();
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
+  if (inject_idx) {
+    for (int i = 0; i < batch; ++i)
+      TD3_ARG(inject_idx[i] >= 0 && inject_idx[i] < r->cap, "injected index out of range");
+    TD3_HIP(hipMemcpyAsync(P->d_inject_idx, inject_idx, (size_t)batch * 8, hipMemcpyHostToDevice, s));
+  }
+  if (inject_noise)
+    TD3_HIP(hipMemcpyAsync(P->noise, inject_noise, (size_t)batch * h->ad * 4, hipMemcpyHostToDevice, s));
+  const int actor_phase = ((h->total_it + 1) % h->cfg.policy_freq) == 0;
+  TD3_RC(input_from_ring(h, r, P, inject_idx != nullptr, s));
+  TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s));
+  if (inject_idx || inject_noise) TD3_HIP(hipStreamSynchronize(s));   // host sources are pageable
+  return finish_step(h, actor_phase, s, stats);
+}
+
+int td3_train_step_batch(td3_handle* h, const float* state, const float* action, const float* next_state,
+                         const float* reward, const float* not_done, int batch, void* stream,
+                         const float* inject_noise, td3_step_stats* stats) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(state && action && next_state && reward && not_done, "null input");
+  TD3_ARG(batch > 0, "batch must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_RC(ensure_plan(h, batch));
+  Plan* P = h->plan.get();
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  if (inject_noise)
+    TD3_HIP(hipMemcpyAsync(P->noise, inject_noise, (size_t)batch * h->ad * 4, hipMemcpyHostToDevice, s));
+  const int actor_phase = ((h->total_it + 1) % h->cfg.policy_freq) == 0;
+  TD3_RC(input_from_batch(h, P, state, action, next_state, reward, not_done, s));
+  TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s));
+  if (inject_noise) TD3_HIP(hipStreamSynchronize(s));
+  return finish_step(h, actor_phase, s, stats);
+}
+
+int td3_select_action(td3_handle* h, const float* state, float* action_out, int n) {
+  TD3_ARG(h && state && action_out, "null argument");
+  TD3_ARG(n > 0, "n must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  ActPlan* A;
+  TD3_RC(build_act(h, pad32(n), &A));
+  hipStream_t s = h->stream;
+  TD3_RC(copy_rows_h2d(A->X_S, pad32(h->sd), 0, state, n, h->sd, s));
+  TD3_RC(run_stages(A->act, s));
+  TD3_HIP(hipMemcpy2DAsync(action_out, (size_t)h->ad * 4, A->X_SP + h->sd, (size_t)pad32(h->sd + h->ad) * 4,
+                           (size_t)h->ad * 4, n, hipMemcpyDeviceToHost, s));
+  TD3_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_out, int n) {
+  TD3_ARG(h && state && action && q_out, "null argument");
+  TD3_ARG(n > 0, "n must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  ActPlan* A;
+  TD3_RC(build_act(h, pad32(n), &A));
+  hipStream_t s = h->stream;
+  const int ld = pad32(h->sd + h->ad);
+  TD3_RC(copy_rows_h2d(A->X_SA, ld, 0, state, n, h->sd, s));
+  TD3_RC(copy_rows_h2d(A->X_SA, ld, h->sd, action, n, h->ad, s));
+  TD3_RC(run_stages(A->evalq, s));
+  TD3_HIP(hipMemcpyAsync(q_out, A->Q[0].Qv, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  TD3_HIP(hipMemcpyAsync(q_out + n, A->Q[1].Qv, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  TD3_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int td3_comm_unique_id(unsigned char out[128]) {
+  TD3_ARG(out != nullptr, "null argument");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    set_error("ncclGetUniqueId: %s", ncclGetErrorString(r));
+    return -2;
+  }
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  memcpy(out, &id, 128);
+  return 0;
+}
+
+int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int rank) {
+  TD3_ARG(h && id, "null argument");
+  TD3_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / nranks");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, 128);
+  ncclComm_t c;
+  ncclResult_t r = ncclCommInitRank(&c, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    set_error("ncclCommInitRank: %s", ncclGetErrorString(r));
+    return -2;
+  }
+  if (h->comm) ncclCommDestroy(h->comm);
+  h->comm = c;
+  h->nranks = nranks;
+  h->rank = rank;
+  if (h->plan) {           // stage lists change (grad write + all-reduce + flat Adam)
+    int B = h->plan->B;
+    TD3_RC(build_step(h, B));
+  }
+  return 0;
+}
+
+int td3_sync(td3_handle* h) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+void* td3_stream(td3_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase, float* ms, int max_stages,
+                       int* n_stages) {
+  TD3_ARG(h && rbh && ms && n_stages, "null argument");
+  Ring* r = reinterpret_cast<Ring*>(rbh);
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_RC(ensure_plan(h, batch));
+  Plan* P = h->plan.get();
+  std::vector<Stage>& st = P->body[actor_phase ? 1 : 0][0];
+  const int n = (int)st.size() + 1;
+  TD3_ARG(max_stages >= n, "max_stages too small");
+  std::vector<hipEvent_t> ev(n + 1);
+  for (auto& e : ev) TD3_HIP(hipEventCreate(&e));
+  hipStream_t s = h->stream;
+  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
+  TD3_HIP(hipEventRecord(ev[0], s));
+  TD3_RC(input_from_ring(h, r, P, false, s));
+  TD3_HIP(hipEventRecord(ev[1], s));
+  for (int i = 0; i < (int)st.size(); ++i) {
+    TD3_RC(st[i].run(s));
+    TD3_HIP(hipEventRecord(ev[i + 2], s));
+  }
+  TD3_HIP(hipStreamSynchronize(s));
+  h->stage_names.clear();
+  h->stage_names.push_back("gather");
+  for (int i = 0; i < n; ++i) {
+    TD3_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+    if (i) h->stage_names.push_back(st[i - 1].name);
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  *n_stages = n;
+  h->last_body = &st;
+  // the profiled step is a real step: keep the host mirror in sync
+  h->total_it += 1;
+  h->critic_step += 1;
+  if (actor_phase) h->actor_step += 1;
+  return 0;
+}
+
+const char* td3_stage_name(td3_handle* h, int i) {
+  if (!h || i < 0 || i >= (int)h->stage_names.size()) return "";
+  return h->stage_names[i].c_str();
+}
+
+double td3_stage_flops(td3_handle* h, int i) {
+  if (!h || !h->last_body || i <= 0 || i > (int)h->last_body->size()) return 0.0;
+  return (*h->last_body)[i - 1].flops;
+}
+
+int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean) {
+  TD3_ARG(h && ms_mean, "null argument");
+  TD3_ARG(h->last_body != nullptr, "run td3_profile_stages first");
+  TD3_ARG(stage >= 1 && stage <= (int)h->last_body->size(), "stage index out of range");
+  TD3_ARG(iters > 0, "iters must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  Stage& st = (*h->last_body)[stage - 1];
+  hipEvent_t a, b;
+  TD3_HIP(hipEventCreate(&a));
+  TD3_HIP(hipEventCreate(&b));
+  hipStream_t s = h->stream;
+  TD3_RC(st.run(s));    // warm
+  TD3_HIP(hipEventRecord(a, s));
+  for (int i = 0; i < iters; ++i) TD3_RC(st.run(s));
+  TD3_HIP(hipEventRecord(b, s));
+  TD3_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  TD3_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_mean = ms / iters;
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,248 @@
+"""HBM-resident replay buffers with the reference's Python surface.
+
+Drop-in for ``/root/reference/my_replay_buffer.py``:
+
+* ``ReplayBuffer_featured(obs_space, action_space, max_size=1e6, load_folder=None)``
+  (:72-89) with ``add`` (:109-117), ``sample`` (:119-128), ``save`` / ``load``
+  (:91-107) and the ``ptr`` / ``size`` / ``max_size`` attributes.
+
+The storage lives in HBM (``libtd3hip``'s ring, one fp32 record per transition).
+``add`` stages rows on the host and ships them in batches (pinned memory, async
+H2D); ``sample`` / ``TD3.train`` flush first, so a transition added at step t is
+samplable at step t exactly as in the reference (main.py:261 before :269).
+``sample`` draws indices with a device Philox stream instead of the global numpy
+MT19937 (``np.random.randint`` at :120) -- a documented, deliberate difference.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+_STAGE_ROWS = 4096
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def default_device_index() -> int:
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise RuntimeError("td3_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"]) % torch.cuda.device_count()
+    return torch.cuda.current_device()
+
+
+class _SafeIntUnpickler(pickle.Unpickler):
+    """ptr.pkl / size.pkl hold a pickled int (my_replay_buffer.py:93-95); refuse anything else."""
+
+    def find_class(self, module, name):
+        raise pickle.UnpicklingError(f"refusing to load {module}.{name} from a buffer file")
+
+
+def _load_int(path):
+    with open(path, "rb") as f:
+        v = _SafeIntUnpickler(f).load()
+    if not isinstance(v, (int, np.integer)):
+        raise ValueError(f"{path}: expected an int, got {type(v)}")
+    return int(v)
+
+
+class ReplayBuffer_featured(object):
+    """Flat-observation replay ring (my_replay_buffer.py:72-128) resident in HBM."""
+
+    store_np = ["state", "action", "next_state", "reward", "not_done"]
+    store_pkl = ["ptr", "size"]
+
+    def __init__(self, obs_space, action_space, max_size=int(1e6), load_folder=None,
+                 device=None, seed=0):
+        self._lib = _lib.load()
+        self.state_dim = int(obs_space.shape[0])
+        self.action_dim = int(action_space.shape[0])
+        self._dev = default_device_index() if device is None else int(device)
+        torch = _torch()
+        self.device = torch.device("cuda", self._dev)
+        self.seed = int(seed)
+        self._h = None
+        self._pending = []
+        if load_folder is not None:
+            self.load(load_folder)
+        else:
+            self._create(int(max_size))
+
+    # ------------------------------------------------------------------ plumbing
+    def _create(self, max_size):
+        import ctypes as C
+        if self._h is not None:
+            self._lib.rb_destroy(self._h)
+            self._h = None
+        h = C.c_void_p()
+        check(self._lib.rb_create(self.state_dim, self.action_dim, max_size, self._dev,
+                                  self.seed, C.byref(h)), "rb_create")
+        self._h = h
+        self.max_size = max_size
+        info = self._info()
+        self.record_floats = info.record_floats
+
+    def _info(self):
+        info = _lib.rb_info_t()
+        check(self._lib.rb_info(self._h, info), "rb_info")
+        return info
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def ptr(self):
+        self.flush()
+        return int(self._info().ptr)
+
+    @property
+    def size(self):
+        self.flush()
+        return int(self._info().size)
+
+    def _stream(self):
+        torch = _torch()
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    # ------------------------------------------------------------------ reference API
+    def add(self, state, action, next_state, reward, done):
+        """my_replay_buffer.py:109-117 (stores not_done = 1 - done)."""
+        self._pending.append((np.asarray(state, dtype=np.float64).reshape(self.state_dim),
+                              np.asarray(action, dtype=np.float64).reshape(self.action_dim),
+                              np.asarray(next_state, dtype=np.float64).reshape(self.state_dim),
+                              float(np.asarray(reward, dtype=np.float64).reshape(-1)[0]),
+                              float(np.asarray(done, dtype=np.float64).reshape(-1)[0])))
+        if len(self._pending) >= _STAGE_ROWS:
+            self.flush()
+
+    def add_batch(self, state, action, next_state, reward, done):
+        """Bulk add of n transitions (experience_injection.py / hindsight relabel path)."""
+        self.flush()
+        s = np.ascontiguousarray(state, dtype=np.float64).reshape(-1, self.state_dim)
+        n = s.shape[0]
+        a = np.ascontiguousarray(action, dtype=np.float64).reshape(n, self.action_dim)
+        s2 = np.ascontiguousarray(next_state, dtype=np.float64).reshape(n, self.state_dim)
+        r = np.ascontiguousarray(reward, dtype=np.float64).reshape(n)
+        d = np.ascontiguousarray(done, dtype=np.float64).reshape(n)
+        check(self._lib.rb_add(self._h, _lib.dptr(s), _lib.dptr(a), _lib.dptr(s2), _lib.dptr(r),
+                               _lib.dptr(d), n, self._stream()), "rb_add")
+
+    def flush(self):
+        if not self._pending:
+            return
+        rows = self._pending
+        self._pending = []
+        s = np.stack([x[0] for x in rows])
+        a = np.stack([x[1] for x in rows])
+        s2 = np.stack([x[2] for x in rows])
+        r = np.array([x[3] for x in rows], dtype=np.float64)
+        d = np.array([x[4] for x in rows], dtype=np.float64)
+        check(self._lib.rb_add(self._h, _lib.dptr(s), _lib.dptr(a), _lib.dptr(s2), _lib.dptr(r),
+                               _lib.dptr(d), len(rows), self._stream()), "rb_add")
+
+    def fill_synthetic(self, n, max_action=1.0, seed=0):
+        """Device-side prefill with the SURVEY §8(d) synthetic distribution (bench/tests)."""
+        self.flush()
+        check(self._lib.rb_fill_synthetic(self._h, int(n), float(max_action), int(seed),
+                                          self._stream()), "rb_fill_synthetic")
+
+    def sample(self, batch_size, indices=None, return_indices=False):
+        """my_replay_buffer.py:119-128: (state, action, next_state, reward, not_done) fp32 on device."""
+        torch = _torch()
+        self.flush()
+        B = int(batch_size)
+        dev = self.device
+        out = (torch.empty((B, self.state_dim), device=dev, dtype=torch.float32),
+               torch.empty((B, self.action_dim), device=dev, dtype=torch.float32),
+               torch.empty((B, self.state_dim), device=dev, dtype=torch.float32),
+               torch.empty((B, 1), device=dev, dtype=torch.float32),
+               torch.empty((B, 1), device=dev, dtype=torch.float32))
+        idx_out = torch.empty((B,), device=dev, dtype=torch.int64)
+        inj = None
+        if indices is not None:
+            inj = torch.as_tensor(np.asarray(indices, dtype=np.int64), device=dev)
+            if inj.numel() != B:
+                raise ValueError("indices must have batch_size entries")
+            size = self.size
+            if B and (int(inj.min()) < 0 or int(inj.max()) >= max(size, 1)):
+                raise IndexError("index out of range of the filled buffer")
+        check(self._lib.rb_sample(self._h, B, *[t.data_ptr() for t in out],
+                                  inj.data_ptr() if inj is not None else None,
+                                  idx_out.data_ptr(), self._stream()), "rb_sample")
+        if return_indices:
+            return out, idx_out
+        return out
+
+    # ------------------------------------------------------------------ persistence
+    def _records(self):
+        n = self.max_size
+        rec = np.empty((n, self.record_floats), dtype=np.float32)
+        check(self._lib.rb_read_records(self._h, 0, n, _lib.fptr(rec)), "rb_read_records")
+        return rec
+
+    def _arrays(self):
+        rec = self._records()
+        sd, ad = self.state_dim, self.action_dim
+        return {
+            "state": rec[:, :sd].astype(np.float64),
+            "action": rec[:, sd:sd + ad].astype(np.float64),
+            "next_state": rec[:, sd + ad:2 * sd + ad].astype(np.float64),
+            "reward": rec[:, 2 * sd + ad:2 * sd + ad + 1].astype(np.float64),
+            "not_done": rec[:, 2 * sd + ad + 1:2 * sd + ad + 2].astype(np.float64),
+        }
+
+    def save(self, folder):
+        """my_replay_buffer.py:91-99: ptr/size pickled (protocol 4), arrays via np.save."""
+        self.flush()
+        os.makedirs(folder, exist_ok=True)
+        info = self._info()
+        for attrib, v in (("ptr", int(info.ptr)), ("size", int(info.size))):
+            with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
+                pickle.dump(v, f, protocol=4)
+        for attrib, arr in self._arrays().items():
+            with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
+                np.save(f, arr)
+
+    def load(self, folder):
+        """my_replay_buffer.py:101-107 (pickles are read by an int-only unpickler)."""
+        ptr = _load_int(os.path.join(folder, "ptr.pkl"))
+        size = _load_int(os.path.join(folder, "size.pkl"))
+        arrs = {}
+        for attrib in self.store_np:
+            with open(os.path.join(folder, attrib + ".pkl"), "rb") as f:
+                arrs[attrib] = np.load(f, allow_pickle=False)
+        n = arrs["state"].shape[0]
+        self.state_dim = arrs["state"].shape[1]
+        self.action_dim = arrs["action"].shape[1]
+        self._create(n)
+        sd, ad = self.state_dim, self.action_dim
+        rec = np.zeros((n, self.record_floats), dtype=np.float32)
+        rec[:, :sd] = arrs["state"]
+        rec[:, sd:sd + ad] = arrs["action"]
+        rec[:, sd + ad:2 * sd + ad] = arrs["next_state"]
+        rec[:, 2 * sd + ad] = arrs["reward"].reshape(n)
+        rec[:, 2 * sd + ad + 1] = arrs["not_done"].reshape(n)
+        check(self._lib.rb_write_records(self._h, 0, n, _lib.fptr(rec), ptr % n, min(size, n)),
+              "rb_write_records")
+
+    def __del__(self):
+        try:
+            if self._h is not None and _lib.alive():
+                self._lib.rb_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+# The reference's module-level alias used by main.py:204-208.
+ReplayBuffer = ReplayBuffer_featured

@@ -1,0 +1,204 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the goldens.
+
+Every test here runs on an MI355X; the oracle (oracle/td3_oracle.py) is the checker.
+Tolerances (fp32): forward values / losses rtol 1e-5 (abs floor 1e-6 of
+the tensor scale), gradients rtol 1e-4, post-Adam parameters within 1e-6 + 1e-5|x| on
+>= 99.9 % of elements and within 2*lr everywhere (sign flips of ~0 gradients).
+"""
+import numpy as np
+import pytest
+
+from helpers import gen, orc, load_golden, featured_setup
+
+pytestmark = pytest.mark.gpu
+
+
+class Box:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+
+
+def _rel_to_max(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / (np.abs(b).max() + 1e-30))
+
+
+def _make(S, use_graph=True):
+    from td3_amd.TD3_featured import TD3
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+    hp = dict(S["hp"])
+    lr = hp.pop("lr", 1e-4)
+    pol = TD3(Box((S["sd"],)), Box((S["ad"],)), max_action=S["ma"], norm=S["norm"], lr=lr,
+              use_graph=use_graph, init="none", **hp)
+    pol.set_weights(S["actor"], S["critic"])
+    rb = ReplayBuffer_featured(Box((S["sd"],)), Box((S["ad"],)), max_size=gen.BUFFER_ROWS)
+    s, a, s2, r, d = gen.fill_featured_buffer(S["sd"], S["ad"], S["ma"], gen.BUFFER_ROWS, gen.SEED)
+    rb.add_batch(s, a, s2, r, d)
+    return pol, rb
+
+
+def _params_close(gpu, ref, lr, what):
+    for k in ref:
+        g, o = np.asarray(gpu[k], np.float64), np.asarray(ref[k], np.float64)
+        err = np.abs(g - o)
+        tight = err <= 1e-6 + 1e-5 * np.abs(o)
+        assert tight.mean() >= 0.999 or (~tight).sum() <= 2, (what, k, (~tight).sum(), err.max())
+        assert err.max() <= 2.5 * lr, (what, k, err.max())
+
+
+def _load_oracle_state(pol, L):
+    pol.set_weights(L.actor, L.critic, L.actor_target, L.critic_target)
+    from td3_amd import _lib
+    from td3_amd.TD3_featured import _ParamView
+    _ParamView(pol, _lib.TD3_ACTOR_ADAM_M, 0).load_state_dict(L.actor_m)
+    _ParamView(pol, _lib.TD3_ACTOR_ADAM_V, 0).load_state_dict(L.actor_v)
+    _ParamView(pol, _lib.TD3_CRITIC_ADAM_M, 1).load_state_dict(L.critic_m)
+    _ParamView(pol, _lib.TD3_CRITIC_ADAM_V, 1).load_state_dict(L.critic_v)
+    pol._set_counters(L.total_it, L.critic_step, L.actor_step)
+
+
+def test_sample_gather_bit_exact():
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    idx = np.random.RandomState(3).randint(0, gen.BUFFER_ROWS, size=300)
+    out = rb.sample(300, indices=idx)
+    ref = S["buf"].gather(idx)
+    for o, r in zip(out, ref):
+        np.testing.assert_array_equal(o.cpu().numpy(), r)
+
+
+def test_sample_philox_uniform_and_in_range():
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    counts = np.zeros(gen.BUFFER_ROWS)
+    for _ in range(40):
+        (s, a, s2, r, nd), idx = rb.sample(1000, return_indices=True)
+        ix = idx.cpu().numpy()
+        assert ix.min() >= 0 and ix.max() < gen.BUFFER_ROWS
+        np.testing.assert_array_equal(s.cpu().numpy(), S["buf"].state[ix].astype(np.float32))
+        counts += np.bincount(ix, minlength=gen.BUFFER_ROWS)
+    # 40k draws over 1000 bins: chi-square within a generous bound
+    e = counts.sum() / counts.size
+    chi2 = ((counts - e) ** 2 / e).sum()
+    assert chi2 < 1200, chi2
+
+
+@pytest.mark.parametrize("name", list(gen.FEATURED_CONFIGS))
+def test_train_step_teacher_forced(name):
+    """Each step starts from the oracle's state; every output of the step is compared."""
+    G = load_golden("featured", name)
+    S = featured_setup(name)
+    pol, rb = _make(S)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    lr = S["kw"].get("lr", 1e-4)
+    for step in range(1, S["steps"] + 1):
+        p = f"step{step}"
+        idx, noise = G[f"{p}/idx"], G[f"{p}/noise"]
+        _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        out = pol.train_step(rb, S["B"], indices=idx, noise=noise, stats=True)
+        np.testing.assert_array_equal(out["idx"], idx)
+        assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5, (p, "y")
+        assert _rel_to_max(out["q1"], rec["q1"][:, 0]) <= 1e-5, (p, "q1")
+        assert _rel_to_max(out["q2"], rec["q2"][:, 0]) <= 1e-5, (p, "q2")
+        np.testing.assert_allclose(out["critic_loss"], rec["critic_loss"], rtol=1e-5)
+        assert out["actor_step"] == ("actor_loss" in rec)
+        if out["actor_step"]:
+            np.testing.assert_allclose(out["actor_loss"], rec["actor_loss"], rtol=1e-5, atol=1e-7)
+        # the same quantities against the reference goldens directly
+        assert _rel_to_max(out["y"], G[f"{p}/y"][:, 0]) <= 2e-5
+        _params_close(pol.critic.numpy_dict(), L.critic, lr, (p, "critic"))
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, lr, (p, "critic_target"))
+        _params_close(pol.actor.numpy_dict(), L.actor, lr, (p, "actor"))
+        _params_close(pol.actor_target.numpy_dict(), L.actor_target, lr, (p, "actor_target"))
+        assert pol._counters() == (L.total_it, L.critic_step, L.actor_step)
+
+
+def test_adam_moments_match_oracle():
+    S = featured_setup("hc_layer")
+    G = load_golden("featured", "hc_layer")
+    pol, rb = _make(S)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    for step in (1, 2):
+        p = f"step{step}"
+        orc.featured_train_step(L, S["buf"].gather(G[f"{p}/idx"]), G[f"{p}/noise"])
+        pol.train_step(rb, S["B"], indices=G[f"{p}/idx"], noise=G[f"{p}/noise"])
+    sd = pol.critic_optimizer.state_dict()
+    assert float(sd["state"][0]["step"]) == 2.0
+    for i, k in enumerate(L.critic):
+        m = sd["state"][i]["exp_avg"].numpy()
+        assert _rel_to_max(m, L.critic_m[k]) <= 2e-4, k
+    sda = pol.actor_optimizer.state_dict()
+    assert float(sda["state"][0]["step"]) == 1.0
+    for i, k in enumerate(L.actor):
+        assert _rel_to_max(sda["state"][i]["exp_avg"].numpy(), L.actor_m[k]) <= 2e-4, k
+
+
+@pytest.mark.parametrize("name", ["hc_layer", "hc_none", "pend_layer"])
+def test_free_running_matches_golden(name):
+    """Four free-running steps against the reference's own goldens."""
+    G = load_golden("featured", name)
+    S = featured_setup(name)
+    pol, rb = _make(S)
+    for step in range(1, S["steps"] + 1):
+        p = f"step{step}"
+        out = pol.train_step(rb, S["B"], indices=G[f"{p}/idx"], noise=G[f"{p}/noise"], stats=True)
+        assert _rel_to_max(out["y"], G[f"{p}/y"][:, 0]) <= 5e-5
+        assert _rel_to_max(out["q1"], G[f"{p}/q1"][:, 0]) <= 5e-5
+        np.testing.assert_allclose(out["critic_loss"], float(G[f"{p}/critic_loss"]), rtol=5e-5)
+        for grp, view, sb in (("actor", pol.actor, 0), ("critic", pol.critic, 500),
+                              ("critic_target", pol.critic_target, 500)):
+            for i, (k, v) in enumerate(view.numpy_dict().items()):
+                st, smp = gen.summarize(v, salt=sb + i)
+                ref = G[f"{p}/{grp}/{k}/samples"]
+                assert np.abs(smp - ref).max() <= 2.5e-4, (p, grp, k)
+
+
+def test_graph_equals_eager():
+    S = featured_setup("hc_layer")
+    G = load_golden("featured", "hc_layer")
+    outs = []
+    for use_graph in (False, True):
+        pol, rb = _make(S, use_graph=use_graph)
+        for step in range(1, 5):
+            p = f"step{step}"
+            pol.train_step(rb, S["B"], indices=G[f"{p}/idx"], noise=G[f"{p}/noise"])
+        outs.append((pol.actor.flat(), pol.critic.flat(), pol.critic_target.flat()))
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_select_action_and_eval_q():
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    rs = np.random.RandomState(0)
+    for _ in range(3):
+        s = rs.standard_normal(S["sd"]).astype(np.float32)
+        a = pol.select_action(s)
+        ref = orc.featured_select_action(S["actor"], S["norm"], S["ma"], s)
+        assert a.dtype == np.float32 and a.shape == (S["ad"],)
+        np.testing.assert_allclose(a, ref, rtol=1e-5, atol=1e-6)
+        q = pol.eval_q(s, a)
+        q1, _ = orc.featured_q(S["critic"], "q1", S["norm"], s[None], a[None])
+        q2, _ = orc.featured_q(S["critic"], "q2", S["norm"], s[None], a[None])
+        np.testing.assert_allclose(q[0], q1[0], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(q[1], q2[0], rtol=1e-5, atol=1e-6)
+
+
+def test_foreign_buffer_path():
+    """A duck-typed buffer (the reference's own class shape) goes through sample() tensors."""
+    S = featured_setup("hc_layer")
+    G = load_golden("featured", "hc_layer")
+    pol, _ = _make(S)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    idx, noise = G["step1/idx"], G["step1/noise"]
+
+    class Foreign:
+        def sample(self, B):
+            import torch
+            return tuple(torch.from_numpy(x) for x in S["buf"].gather(idx))
+
+    rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+    out = pol.train_step(Foreign(), S["B"], noise=noise, stats=True)
+    assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5
+    _params_close(pol.critic.numpy_dict(), L.critic, 1e-4, "critic")
