@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""TD3 gradient-steps/s on MI355X (BASELINE.json metric), HalfCheetah-v4 shapes, batch 256/GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one ``TD3.train(replay_buffer, 256)`` call (TD3_featured.py:123-171): Philox
+index draw + HBM gather from a 1e6-row replay ring pre-filled with synthetic transitions
+(SURVEY.md §8d), the twin-critic update and, every policy_freq=2 steps, the actor update +
+Polyak.  N GPUs = data parallel: every rank owns a replay shard and samples its own 256
+rows; gradients are all-reduced over RCCL (xGMI) before Adam.  ``value`` counts
+batch-256 gradient steps over all ranks (weak scaling).
+
+Prints ONE JSON line on rank 0 (the driver contract) with a ``roofline`` object for the
+dominant kernel (HIP-event timed live) and a ``cpu_baseline`` (the numpy oracle on the
+host cores, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SD, AD, MAX_ACTION, BATCH, REPLAY = 17, 6, 1.0, 256, 1_000_000
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8 TB/s spec
+FP32_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: f32 MFMA / vector peak
+
+
+class Box:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+
+
+def stage_table(pol, rb, iters=50):
+    """Per-stage mean device time (HIP events, handle stream) for an odd and an even step."""
+    lib, h = pol._lib, pol._h
+    rows = []
+    ms = (C.c_float * 128)()
+    n = C.c_int()
+    for phase in (0, 1):
+        rc = lib.td3_profile_stages(h, rb.handle, BATCH, phase, ms, 128, C.byref(n))
+        if rc:
+            raise RuntimeError(lib.td3_last_error().decode())
+        names = [lib.td3_stage_name(h, i).decode() for i in range(n.value)]
+        kernels = [lib.td3_stage_kernel(h, i).decode() for i in range(n.value)]
+        flops = [lib.td3_stage_flops(h, i) for i in range(n.value)]
+        for i in range(1, n.value):
+            if names[i].endswith("_allreduce"):
+                continue          # a collective cannot be re-launched on its own
+            t = C.c_float()
+            rc = lib.td3_time_stage(h, i, iters, C.byref(t))
+            if rc:
+                raise RuntimeError(lib.td3_last_error().decode())
+            rows.append(dict(phase=phase, stage=names[i], kernel=kernels[i],
+                             ms=float(t.value), flops=float(flops[i])))
+    return rows
+
+
+def roofline_from_stages(rows, pmc):
+    """Dominant kernel over one odd + one even step; achieved = algorithmic FLOP / time."""
+    fam = {}
+    for r in rows:
+        f = fam.setdefault(r["kernel"], {"ms": 0.0, "flops": 0.0, "launches": 0})
+        f["ms"] += r["ms"]
+        f["flops"] += r["flops"]
+        f["launches"] += 1
+    dom = max((k for k in fam if k != "rccl"), key=lambda k: fam[k]["ms"])
+    f = fam[dom]
+    per_launch_flops = f["flops"] / f["launches"]
+    per_launch_s = f["ms"] / f["launches"] * 1e-3
+    achieved = per_launch_flops / per_launch_s / 1e12 if f["flops"] > 0 else 0.0
+    traffic = None
+    if pmc and dom in pmc.get("kernels", {}):
+        traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
+    return {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 3),
+            "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+            "traffic": traffic, "launches_per_2_steps": f["launches"],
+            "avg_launch_us": round(per_launch_s * 1e6, 3),
+            "flops_per_launch": per_launch_flops}, fam
+
+
+def cpu_baseline(seconds=12.0):
+    """The numpy oracle (oracle/td3_oracle.py, a restatement of TD3_featured.train pinned to
+    the reference's goldens) on this host's cores: same shapes, B=256."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import gen
+    from oracle import td3_oracle as orc
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    a0 = gen.init_params(gen.featured_actor_shapes(SD, AD, "layer"), 1)
+    c0 = gen.init_params(gen.featured_critic_shapes(SD, AD, "layer"), 2)
+    L = orc.Learner(a0, c0, max_action=MAX_ACTION, norm="layer")
+    rows = 20000
+    buf = orc.FeaturedBuffer(SD, AD, rows)
+    rs = np.random.RandomState(0)
+    buf.state[:] = rs.standard_normal((rows, SD))
+    buf.action[:] = rs.uniform(-1, 1, (rows, AD))
+    buf.next_state[:] = rs.standard_normal((rows, SD))
+    buf.reward[:] = rs.standard_normal((rows, 1))
+    buf.not_done[:] = (rs.uniform(size=(rows, 1)) > 0.01)
+    buf.size = rows
+    steps = 0
+    orc.featured_train_step(L, buf.gather(rs.randint(0, rows, BATCH)),
+                            rs.standard_normal((BATCH, AD)).astype(np.float32))  # warm
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds or steps < 4:
+        idx = rs.randint(0, rows, BATCH)
+        noise = rs.standard_normal((BATCH, AD)).astype(np.float32)
+        orc.featured_train_step(L, buf.gather(idx), noise)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 3), "unit": "grad-steps/s", "cores": int(cores),
+            "kind": "port",
+            "sample": f"{steps} oracle train steps (HalfCheetah dims, B=256, norm=layer) in {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="disable hipGraph replay")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from td3_amd import _lib
+    from td3_amd.TD3_featured import TD3
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+
+    torch.manual_seed(1000 + rank if world == 1 else 1000)   # same init on every rank
+    pol = TD3(Box((SD,)), Box((AD,)), max_action=MAX_ACTION, norm="layer", device=local,
+              seed=17 + rank, use_graph=not args.eager)
+    rb = ReplayBuffer_featured(Box((SD,)), Box((AD,)), max_size=REPLAY, device=local, seed=101 + rank)
+    rb.fill_synthetic(REPLAY, MAX_ACTION, seed=7 + rank)
+    if world > 1:
+        uid = (C.c_ubyte * 128)()
+        t = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            _lib.check(pol._lib.td3_comm_unique_id(uid), "td3_comm_unique_id")
+            t.copy_(torch.tensor(list(bytes(uid)), dtype=torch.uint8))
+        dist.broadcast(t, 0)
+        uid = (C.c_ubyte * 128)(*t.cpu().tolist())
+        _lib.check(pol._lib.td3_comm_init(pol._h, uid, world, rank), "td3_comm_init")
+
+    def barrier_sync():
+        pol.sync()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        pol.train(rb, BATCH)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pol.train(rb, BATCH)
+    pol.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    rows, fam, roof = None, None, None
+    if not args.no_roofline:           # every rank runs it: profiled steps contain collectives
+        rows = stage_table(pol, rb)
+        if rank == 0:
+            pmc = None
+            pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc_path):
+                with open(pmc_path) as f:
+                    pmc = json.load(f)
+            roof, fam = roofline_from_stages(rows, pmc)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        gsteps = args.steps / dt
+        value = world * gsteps
+        out = {
+            "metric": "TD3 gradient-steps/sec @ batch 256, HalfCheetah-v4, 1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "grad-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (replay ring pre-filled on device: s,s' ~ N(0,1), a ~ U(-1,1), "
+                    "r ~ N(0,1), not_done ~ Bernoulli(0.99); torch-default random init)",
+            "config": {"workload": "TD3_featured.train(replay_buffer, 256) on HalfCheetah-v4 shapes "
+                                   "(state 17, action 6, actor 500-400-300, critic 2x 500-400-200, "
+                                   "LayerNorm, policy_freq 2), replay 1e6 per GPU",
+                       "global_batch": BATCH * world, "per_gpu_batch": BATCH, "replay_per_gpu": REPLAY,
+                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "global_steps_per_s": round(gsteps, 2),
+                       "graph": not args.eager},
+        }
+        if roof is not None:
+            out["roofline"] = roof
+            out["stage_us"] = {f"{r['phase']}:{r['stage']}": round(r["ms"] * 1e3, 2) for r in rows}
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,18 +1,24 @@
 // TD3 gradient-step kernels for gfx950 (MI355X).
 //
 // What each kernel restates (reference = /root/reference):
-//   gemm_kernel<0,*>      nn.Linear forward + ReLU, with the previous layer's
-//                         LayerNorm (ReLU -> LN order, TD3_featured.py:41-46 / :75-80)
-//                         applied to the input rows in the prologue
-//   gemm_kernel<1,*>      dX = dZ * W of a Linear, with LN-backward + ReLU-backward
-//                         of the following layer applied to the dZ rows in the prologue
-//   head_kernel           last LN + output Linear + {target smoothing :131-137,
-//                         max_action*tanh :47-48, Q value :81}
-//   critic_loss_kernel    min(Q1',Q2'), y = r + nd*gamma*min (:140-142), mse grads (:148)
-//   actor_loss_kernel     -mean(Q1(s, pi(s))) backward into LN3 (:159)
-//   actor_head_bwd_kernel dQ1/da -> tanh / max_action backward -> actor head backward
-//   dw_kernel             weight / bias / LN-affine grads (batch reductions) fused
-//                         with torch Adam (adam.py:457-547) and Polyak (:167-171)
+//   gemm_kernel<0,*,P>   nn.Linear forward + ReLU of one layer for several networks; the
+//                        prologue P builds the input rows: copy, the previous layer's
+//                        LayerNorm (ReLU -> LN order, TD3_featured.py:41-46 / :75-80), or a
+//                        fused head (target smoothing :131-137, pi = max_action*tanh :47-48)
+//   gemm_kernel<1,*,P>   dX = dZ * W of a Linear; the prologue forms dZ from dU
+//                        (LN backward + ReLU backward) or from a fused loss head
+//                        (clipped double-Q target + mse grads :139-148, -mean Q1 :159,
+//                        dQ1/da -> tanh / max_action backward -> actor head)
+//   dw_kernel            weight / bias / LN-affine grads (batch reductions, MFMA) fused
+//                        with torch Adam (adam.py:457-547) and Polyak (:167-171)
+//   lnbwd_rows_kernel    dZ of the first hidden layer (no GEMM follows it)
+//   head_kernel          act / eval_q heads (TD3_featured.py:113-121)
+//
+// Latency rules applied everywhere (every kernel here is latency-bound at B=256):
+// every operand a workgroup needs is requested before the first wait (weight fragments
+// for all of a wave's K chunks, all rows of a batch, LN affines, head weights); wave
+// reductions use DPP + readlane (no LDS round trips); rows are processed in batches so
+// independent reductions interleave.
 //
 // Compute dtype: fp32 everywhere.  Matrix products use v_mfma_f32_32x32x2_f32
 // (exact fp32 FMA chain, MI355X_MICROARCH.md § Matrix cores).
@@ -23,125 +29,619 @@
 namespace td3 {
 
 // ================================================================== helpers
-template <int Q>
-__device__ __forceinline__ void ln_stats(const float (&x)[Q], int K, int lane, float& mean,
-                                         float& rstd) {
-  float s = 0.f;
-#pragma unroll
-  for (int q = 0; q < Q; ++q)
-    if (lane + 64 * q < K) s += x[q];
-  s = wave_sum(s);
-  mean = s / (float)K;
-  float v = 0.f;
-#pragma unroll
-  for (int q = 0; q < Q; ++q)
-    if (lane + 64 * q < K) {
-      float d = x[q] - mean;
-      v += d * d;
-    }
-  v = wave_sum(v) / (float)K;
-  rstd = 1.0f / sqrtf(v + 1e-5f);
+// Wave64 sum, result uniform: DPP within each 16-lane row, then the four rows via readlane.
+__device__ __forceinline__ float wsum(float v) {
+  int x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false)); // row_half_mirror
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false)); // row_mirror
+  x = __float_as_int(v);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(x, 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(x, 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(x, 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(x, 48));
+  return (r0 + r1) + (r2 + r3);
 }
 
-// dH of LayerNorm followed by the ReLU mask, for one row held as x[q] (col lane+64q).
-// gx = gu*gamma; dh = rstd*((gx - mean(gx)) - xhat*mean(gx*xhat)); dz = h>0 ? dh : 0.
-template <int Q>
-__device__ __forceinline__ void ln_relu_bwd(const float (&gu)[Q], const float (&h)[Q],
-                                            const float* __restrict__ gam, int K, int lane,
-                                            float mean, float rstd, int norm, float (&gz)[Q]) {
+// Global-address-space accessors: pointers read from problem tables are generic to the
+// compiler, which would otherwise emit flat_* loads (counted on vmcnt AND lgkmcnt, so
+// every s_load wait also drains them).  These force global_load / global_store.
+#define GAS __attribute__((address_space(1)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 gld4(const float* p) {
+  const f32x4 v = *(const GAS f32x4*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float gld(const float* p) { return *(const GAS float*)p; }
+__device__ __forceinline__ void gst4(float* p, float4 v) {
+  f32x4 w;
+  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+  *(GAS f32x4*)p = w;
+}
+__device__ __forceinline__ void gst(float* p, float v) { *(GAS float*)p = v; }
+
+// A lane's slice of a row of width <= 512: v[4q+e] = row[lane*4 + 256q + e].
+__device__ __forceinline__ int rcol(int lane, int j) { return lane * 4 + ((j >> 2) << 8) + (j & 3); }
+
+__device__ __forceinline__ void rv_load(float (&v)[8], const float* __restrict__ row, int n, int lane) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  const float4 a = gld4(row + (c0 < n ? c0 : 0));
+  const float4 b = gld4(row + (c1 < n ? c1 : 0));
+  const bool va = c0 < n, vb = c1 < n;
+  v[0] = va ? a.x : 0.f; v[1] = va ? a.y : 0.f; v[2] = va ? a.z : 0.f; v[3] = va ? a.w : 0.f;
+  v[4] = vb ? b.x : 0.f; v[5] = vb ? b.y : 0.f; v[6] = vb ? b.z : 0.f; v[7] = vb ? b.w : 0.f;
+}
+
+__device__ __forceinline__ void rv_store(float* __restrict__ row, int n, int lane, const float (&v)[8]) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  if (c0 < n) gst4(row + c0, make_float4(v[0], v[1], v[2], v[3]));
+  if (c1 < n) gst4(row + c1, make_float4(v[4], v[5], v[6], v[7]));
+}
+
+__device__ __forceinline__ void rv_load_lds(float (&v)[8], const float* row, int n, int lane) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  const float4 a = *reinterpret_cast<const float4*>(row + (c0 < n ? c0 : 0));
+  const float4 b = *reinterpret_cast<const float4*>(row + (c1 < n ? c1 : 0));
+  const bool va = c0 < n, vb = c1 < n;
+  v[0] = va ? a.x : 0.f; v[1] = va ? a.y : 0.f; v[2] = va ? a.z : 0.f; v[3] = va ? a.w : 0.f;
+  v[4] = vb ? b.x : 0.f; v[5] = vb ? b.y : 0.f; v[6] = vb ? b.z : 0.f; v[7] = vb ? b.w : 0.f;
+}
+
+// LDS row store (generic float4 store into shared memory).
+__device__ __forceinline__ void lds_store8(float* row, int n, int lane, const float (&v)[8]) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  if (c0 < n) *reinterpret_cast<float4*>(row + c0) = make_float4(v[0], v[1], v[2], v[3]);
+  if (c1 < n) *reinterpret_cast<float4*>(row + c1) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+__device__ __forceinline__ float rv_psum(const float (&v)[8], int K, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (rcol(lane, j) < K) s += v[j];
+  return s;
+}
+
+__device__ __forceinline__ float rv_pdot(const float (&a)[8], const float (&b)[8], int K, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (rcol(lane, j) < K) s += a[j] * b[j];
+  return s;
+}
+
+// LayerNorm (torch CPU formula: y = (x*rstd + (-mean*rstd))*gamma + beta), RB rows at once.
+template <int RB>
+__device__ __forceinline__ void ln_fwd_rows(float (&x)[RB][8], const float (&g)[8], const float (&bb)[8],
+                                            int K, int lane, float (&mean)[RB], float (&rstd)[RB]) {
+  float s[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) s[r] = rv_psum(x[r], K, lane);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) mean[r] = wsum(s[r]) / (float)K;
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (rcol(lane, j) < K) {
+        const float d = x[r][j] - mean[r];
+        v += d * d;
+      }
+    s[r] = v;
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rstd[r] = 1.0f / sqrtf(wsum(s[r]) / (float)K + 1e-5f);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const float nb = -mean[r] * rstd[r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      x[r][j] = rcol(lane, j) < K ? (x[r][j] * rstd[r] + nb) * g[j] + bb[j] : 0.f;
+  }
+}
+
+// dZ = relu'(h) * LN_bwd(dU): gx = gu*gamma; dh = rstd*((gx - mean(gx)) - xhat*mean(gx*xhat)).
+template <int RB>
+__device__ __forceinline__ void ln_bwd_rows(float (&gu)[RB][8], const float (&h)[RB][8], const float (&g)[8],
+                                            const float (&mean)[RB], const float (&rstd)[RB], int K,
+                                            int lane, int norm) {
   if (!norm) {
 #pragma unroll
-    for (int q = 0; q < Q; ++q) gz[q] = h[q] > 0.f ? gu[q] : 0.f;
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gu[r][j] = h[r][j] > 0.f ? gu[r][j] : 0.f;
     return;
   }
-  float gx[Q], xh[Q];
-  float s1 = 0.f, s2 = 0.f;
+  float xh[RB][8], s1[RB], s2[RB];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int c = lane + 64 * q;
-    if (c < K) {
-      xh[q] = (h[q] - mean) * rstd;
-      gx[q] = gu[q] * gam[c];
-      s1 += gx[q];
-      s2 += gx[q] * xh[q];
-    } else {
-      xh[q] = 0.f;
-      gx[q] = 0.f;
+  for (int r = 0; r < RB; ++r) {
+    s1[r] = 0.f;
+    s2[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xh[r][j] = (h[r][j] - mean[r]) * rstd[r];
+      gu[r][j] = gu[r][j] * g[j];
+      if (rcol(lane, j) < K) {
+        s1[r] += gu[r][j];
+        s2[r] += gu[r][j] * xh[r][j];
+      }
     }
   }
-  const float m1 = wave_sum(s1) / (float)K;
-  const float m2 = wave_sum(s2) / (float)K;
+  float m1[RB], m2[RB];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const float dh = rstd * ((gx[q] - m1) - xh[q] * m2);
-    gz[q] = (h[q] > 0.f && lane + 64 * q < K) ? dh : 0.f;
+  for (int r = 0; r < RB; ++r) {
+    m1[r] = wsum(s1[r]) / (float)K;
+    m2[r] = wsum(s2[r]) / (float)K;
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      gu[r][j] = (h[r][j] > 0.f && rcol(lane, j) < K) ? rstd[r] * ((gu[r][j] - m1[r]) - xh[r][j] * m2[r])
+                                                      : 0.f;
+}
+
+__device__ __forceinline__ void lds_put_row(float* smem, int S, int row, int Kp, int lane, const float (&v)[8]) {
+  lds_store8(smem + row * S, Kp, lane, v);
+}
+
+// ================================================================== prologues
+// Each writes rows wave*8 .. wave*8+7 of the workgroup's A tile (LDS, [32][S]).
+struct Ctx {
+  int m0, wave, lane, nt, Bp, S;
+};
+
+template <int RB>
+__device__ __forceinline__ void pro_copy(const GemmProb& P, float* smem, const Ctx& c) {
+#pragma unroll
+  for (int r0 = 0; r0 < 8; r0 += RB) {
+    float x[RB][8];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+      rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * 8 + r0 + r) * P.lda, P.Kp, c.lane);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * 8 + r0 + r, P.Kp, c.lane, x[r]);
   }
 }
 
-// Head value: LN(h) . w + b over one row (Q cols per lane); returns the full sum on every lane.
-template <int Q>
-__device__ __forceinline__ float head_dot(const float (&x)[Q], int K, int lane,
-                                          const float* __restrict__ g, const float* __restrict__ bb,
-                                          const float* __restrict__ w, float bias) {
-  float u[Q];
-  if (g) {
-    float mean, rstd;
-    ln_stats<Q>(x, K, lane, mean, rstd);
-    const float nb = -mean * rstd;
+__device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = 8;
+  float x[RB][8], g[8], bb[8], mean[RB], rstd[RB];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int c = lane + 64 * q;
-      u[q] = c < K ? (x[q] * rstd + nb) * g[c] + bb[c] : 0.f;
+  for (int r = 0; r < RB; ++r)
+    rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * 8 + r) * P.lda, P.Kp, c.lane);
+  rv_load(g, P.lng, P.Kp, c.lane);
+  rv_load(bb, P.lnb, P.Kp, c.lane);
+  ln_fwd_rows<RB>(x, g, bb, P.Kreal, c.lane, mean, rstd);
+  const bool t0 = c.nt == 0;
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int row = c.wave * 8 + r, grow = c.m0 + row;
+    lds_put_row(smem, c.S, row, P.Kp, c.lane, x[r]);
+    if (t0 && P.Aout) rv_store(P.Aout + (size_t)grow * P.ldao, P.Kp, c.lane, x[r]);
+    if (t0 && P.stats && c.lane == 0) {
+      gst(P.stats + (grow), mean[r]);
+      gst(P.stats + (c.Bp + grow), rstd[r]);
     }
-  } else {
-#pragma unroll
-    for (int q = 0; q < Q; ++q) u[q] = x[q];
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int c = lane + 64 * q;
-    if (c < K) s += u[q] * w[c];
-  }
-  return wave_sum(s) + bias;
-}
-
-constexpr int QR = 8;   // row-kernel columns per lane: rows up to 512 wide
-
-template <int Q>
-__device__ __forceinline__ void load_row(const float* __restrict__ p, int K, int lane, float (&x)[Q]) {
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int c = lane + 64 * q;
-    x[q] = c < K ? p[c] : 0.f;
   }
 }
 
-template <int Q>
-__device__ __forceinline__ void store_row(float* __restrict__ p, int ld, int lane, const float (&x)[Q]) {
+__device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = 2;
+  float g[8];
+  rv_load(g, P.lng, P.Kp, c.lane);
+  const bool t0 = c.nt == 0;
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int c = lane + 64 * q;
-    if (c < ld) p[c] = x[q];
+  for (int r0 = 0; r0 < 8; r0 += RB) {
+    float gu[RB][8], h[RB][8], mean[RB], rstd[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int grow = c.m0 + c.wave * 8 + r0 + r;
+      rv_load(gu[r], P.A + (size_t)grow * P.lda, P.Kp, c.lane);
+      rv_load(h[r], P.H + (size_t)grow * P.ldh, P.Kp, c.lane);
+      mean[r] = P.norm ? gld(P.stats + (grow)) : 0.f;
+      rstd[r] = P.norm ? gld(P.stats + (c.Bp + grow)) : 1.f;
+    }
+    ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.Kreal, c.lane, P.norm);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = c.wave * 8 + r0 + r;
+      lds_put_row(smem, c.S, row, P.Kp, c.lane, gu[r]);
+      if (t0 && P.Aout) rv_store(P.Aout + (size_t)(c.m0 + row) * P.ldao, P.Kp, c.lane, gu[r]);
+    }
+  }
+}
+
+// ---- fused heads of a policy network (target smoothing / pi(s)) -------------------------
+// ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=W4 ex[4]=b4 ex[5]=noise ex[6]=state rows
+// ex[7]=T out ex[8]=U3 out ex[9]=stats3 out
+// exi[0]=K3 exi[1]=ld3 exi[2]=ldw4 exi[3]=ld_state exi[4]=gen_noise exi[5]=ad exi[6]=sd exi[7]=ldn
+// exf[0]=max_action exf[1]=policy_noise exf[2]=noise_clip
+template <bool TARGET>
+__device__ __forceinline__ void pro_policy_head(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = 4;
+  const int K3 = P.exi[0], ld3 = P.exi[1], ldw4 = P.exi[2], lds = P.exi[3];
+  const int ad = P.exi[5], sd = P.exi[6];
+  const float ma = P.exf[0];
+  float g[8], bb[8];
+  if (P.norm) {
+    rv_load(g, P.ex[1], ld3, c.lane);
+    rv_load(bb, P.ex[2], ld3, c.lane);
+  }
+  constexpr int OM = 8;                 // head outputs kept in registers (ad <= 8 fast path)
+  float w4[OM][8], b4v[OM];
+#pragma unroll
+  for (int o = 0; o < OM; ++o) {
+    const int oo = o < ad ? o : 0;
+    rv_load(w4[o], P.ex[3] + (size_t)oo * ldw4, ldw4, c.lane);
+    b4v[o] = gld(P.ex[4] + oo);
+  }
+  const bool t0 = c.nt == 0;
+#pragma unroll
+  for (int r0 = 0; r0 < 8; r0 += RB) {
+    float x[RB][8], st[RB][8], mean[RB], rstd[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int grow = c.m0 + c.wave * 8 + r0 + r;
+      rv_load(x[r], P.ex[0] + (size_t)grow * ld3, ld3, c.lane);
+      rv_load(st[r], P.ex[6] + (size_t)grow * lds, lds, c.lane);
+    }
+    if (P.norm) ln_fwd_rows<RB>(x, g, bb, K3, c.lane, mean, rstd);
+    // head Linear: z_o = u . W4[o] + b4[o]; lane o keeps output o
+    float mine[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) mine[r] = 0.f;
+#pragma unroll
+    for (int o = 0; o < OM; ++o) {
+      if (o < ad) {
+        float s[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) s[r] = rv_pdot(x[r], w4[o], K3, c.lane);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const float z = wsum(s[r]) + b4v[o];
+          if (c.lane == o) mine[r] = z;
+        }
+      }
+    }
+    for (int o = OM; o < ad; ++o) {                 // wide action spaces (ad > 8)
+      float w[8];
+      rv_load(w, P.ex[3] + (size_t)o * ldw4, ldw4, c.lane);
+      const float bo = gld(P.ex[4] + o);
+      float s[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) s[r] = rv_pdot(x[r], w, K3, c.lane);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const float z = wsum(s[r]) + bo;
+        if (c.lane == o) mine[r] = z;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = c.wave * 8 + r0 + r, grow = c.m0 + row;
+      const bool live = grow < P.B;
+      float a = 0.f;
+      if (c.lane < ad) {
+        const int o = c.lane;
+        const float th = tanhf(mine[r]);
+        if (TARGET) {
+          float z;
+          if (P.exi[4]) {                                     // Philox N(0,1) (randn_like, :132)
+            float g4[4];
+            philox_normal4(P.seed, (uint64_t)P.ctr->total_it, kStreamNoise,
+                           (uint32_t)(grow * 8 + (o >> 2)), g4);
+            z = g4[o & 3];
+            if (t0) gst(P.ex[5] + ((size_t)grow * P.exi[7] + o), z);
+          } else {
+            z = gld(P.ex[5] + ((size_t)grow * P.exi[7] + o));
+          }
+          float n = z * P.exf[1];
+          n = fminf(fmaxf(n, -P.exf[2]), P.exf[2]);
+          float v = ma * th + n;                              // TD3_featured.py:135-137
+          a = fminf(fmaxf(v, -ma), ma);
+        } else {
+          a = ma * th;                                        // TD3_featured.py:47-48
+          if (t0) gst(P.ex[7] + ((size_t)grow * 32 + o), th);
+        }
+        if (!live) a = 0.f;
+      }
+      // A row = [state | action | 0]
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = rcol(c.lane, j);
+        const int o = col - sd;
+        const float av = __shfl(a, o >= 0 && o < 64 ? o : 0, 64);
+        v[j] = col < sd ? st[r][j] : (o < ad ? av : 0.f);
+      }
+      lds_put_row(smem, c.S, row, P.Kp, c.lane, v);
+      if (!TARGET && t0) {
+        if (P.norm) rv_store(P.ex[8] + (size_t)grow * ld3, ld3, c.lane, x[r]);
+        if (P.norm && c.lane == 0) {
+          gst(P.ex[9] + (grow), mean[r]);
+          gst(P.ex[9] + (c.Bp + grow), rstd[r]);
+        }
+      }
+    }
+  }
+}
+
+// ---- clipped double-Q target + critic mse backward into LN3 of Q_j -----------------------
+// ex[0..2]=H3 of (target q1, target q2, online q_j)  ex[3..5]=gamma3  ex[6..8]=beta3
+// ex[9..11]=w4 (row 0)  ex[12..14]=b4  ex[15]=reward  ex[16]=not_done
+// out: ex[17]=dZ4_j (ld 32) ex[18]=dU3_j ex[19]=U3_j ex[20]=stats3_j ex[21]=y ex[22]=sqerr_j ex[23]=Q_j
+// exi[0]=K3 exi[1]=ld3 exi[2]=j   exf[0]=discount exf[1]=2/B
+__device__ __forceinline__ void pro_critic_loss(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = 2;
+  const int K3 = P.exi[0], ld3 = P.exi[1], j = P.exi[2];
+  float g[3][8], bb[3][8], w[3][8];
+#pragma unroll
+  for (int n = 0; n < 3; ++n) {
+    if (P.norm) {
+      rv_load(g[n], P.ex[3 + n], ld3, c.lane);
+      rv_load(bb[n], P.ex[6 + n], ld3, c.lane);
+    }
+    rv_load(w[n], P.ex[9 + n], ld3, c.lane);
+  }
+  const float b40 = gld(P.ex[12] + (0)), b41 = gld(P.ex[13] + (0)), b4q = gld(P.ex[14] + (0));
+  const bool t0 = c.nt == 0;
+#pragma unroll
+  for (int r0 = 0; r0 < 8; r0 += RB) {
+    float x0[RB][8], x1[RB][8], xq[RB][8], h[RB][8];
+    float m0[RB], s0[RB], m1[RB], s1[RB], mq[RB], sq[RB], rw[RB], nd[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int grow = c.m0 + c.wave * 8 + r0 + r;
+      rv_load(x0[r], P.ex[0] + (size_t)grow * ld3, ld3, c.lane);
+      rv_load(x1[r], P.ex[1] + (size_t)grow * ld3, ld3, c.lane);
+      rv_load(xq[r], P.ex[2] + (size_t)grow * ld3, ld3, c.lane);
+      rw[r] = gld(P.ex[15] + (grow));
+      nd[r] = gld(P.ex[16] + (grow));
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) h[r][jj] = xq[r][jj];
+    if (P.norm) {
+      ln_fwd_rows<RB>(x0, g[0], bb[0], K3, c.lane, m0, s0);
+      ln_fwd_rows<RB>(x1, g[1], bb[1], K3, c.lane, m1, s1);
+      ln_fwd_rows<RB>(xq, g[2], bb[2], K3, c.lane, mq, sq);
+    }
+    float d0[RB], d1[RB], dq[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      d0[r] = rv_pdot(x0[r], w[0], K3, c.lane);
+      d1[r] = rv_pdot(x1[r], w[1], K3, c.lane);
+      dq[r] = rv_pdot(xq[r], w[2], K3, c.lane);
+    }
+    float gu[RB][8];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = c.wave * 8 + r0 + r, grow = c.m0 + row;
+      const float tq0 = wsum(d0[r]) + b40, tq1 = wsum(d1[r]) + b41, q = wsum(dq[r]) + b4q;
+      const float y = rw[r] + (nd[r] * P.exf[0]) * fminf(tq0, tq1);   // :141-142
+      const float d = q - y;
+      const bool live = grow < P.B;
+      const float gq = live ? P.exf[1] * d : 0.f;                   // mse_loss backward (:148)
+      if (t0 && c.lane == 0) {
+        gst(P.ex[17] + ((size_t)grow * 32), gq);
+        gst(P.ex[23] + grow, q);
+        gst(P.ex[22] + (grow), live ? d * d : 0.f);
+        if (j == 0) gst(P.ex[21] + (grow), y);
+        if (P.norm) {
+          gst(P.ex[20] + (grow), mq[r]);
+          gst(P.ex[20] + (c.Bp + grow), sq[r]);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) gu[r][jj] = gq * w[2][jj];
+      if (t0) {
+        rv_store(P.ex[18] + (size_t)grow * ld3, ld3, c.lane, gu[r]);
+        if (P.norm) rv_store(P.ex[19] + (size_t)grow * ld3, ld3, c.lane, xq[r]);
+      }
+    }
+    ln_bwd_rows<RB>(gu, h, g[2], mq, sq, K3, c.lane, P.norm);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = c.wave * 8 + r0 + r;
+      lds_put_row(smem, c.S, row, P.Kp, c.lane, gu[r]);
+      if (t0 && P.Aout) rv_store(P.Aout + (size_t)(c.m0 + row) * P.ldao, P.Kp, c.lane, gu[r]);
+    }
+  }
+}
+
+// ---- actor loss -mean Q1(s, pi(s)) backward into LN3 of Q1 --------------------------------
+// ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=w4 ex[4]=b4 out ex[5]=Q values
+// exi[0]=K3 exi[1]=ld3   exf[0]=-1/B
+__device__ __forceinline__ void pro_actor_loss(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = 4;
+  const int K3 = P.exi[0], ld3 = P.exi[1];
+  float g[8], bb[8], w[8];
+  if (P.norm) {
+    rv_load(g, P.ex[1], ld3, c.lane);
+    rv_load(bb, P.ex[2], ld3, c.lane);
+  }
+  rv_load(w, P.ex[3], ld3, c.lane);
+  const float b4 = gld(P.ex[4] + (0));
+#pragma unroll
+  for (int r0 = 0; r0 < 8; r0 += RB) {
+    float x[RB][8], h[RB][8], mean[RB], rstd[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+      rv_load(x[r], P.ex[0] + (size_t)(c.m0 + c.wave * 8 + r0 + r) * ld3, ld3, c.lane);
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) h[r][jj] = x[r][jj];
+    if (P.norm) ln_fwd_rows<RB>(x, g, bb, K3, c.lane, mean, rstd);
+    float s[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) s[r] = rv_pdot(x[r], w, K3, c.lane);
+    float gu[RB][8];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int grow = c.m0 + c.wave * 8 + r0 + r;
+      const float q = wsum(s[r]) + b4;
+      if (c.nt == 0 && c.lane == 0) gst(P.ex[5] + (grow), q);
+      const float gq = grow < P.B ? P.exf[0] : 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) gu[r][jj] = gq * w[jj];
+    }
+    ln_bwd_rows<RB>(gu, h, g, mean, rstd, K3, c.lane, P.norm);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * 8 + r0 + r, P.Kp, c.lane, gu[r]);
+  }
+}
+
+// ---- dQ1/da through Q1's first layer, then the actor's head and LN3 backward -------------
+// ex[0]=dU0 of Q1(s,pi) ex[1]=H0 of Q1(s,pi) ex[2]=stats0 ex[3]=gamma0(q1) ex[4]=W1(q1)
+// ex[5]=T (tanh out) ex[6]=W4(actor) ex[7]=H3(actor) ex[8]=stats3(actor) ex[9]=gamma3(actor)
+// out: ex[10]=dZ4 actor (ld 32) ex[11]=dU3 actor
+// exi[0]=K0 exi[1]=ld0 exi[2]=ldw1 exi[3]=sd exi[4]=ad exi[5]=K3 exi[6]=ld3 exi[7]=ldw4
+// exf[0]=max_action
+// The action columns of W1 ([ad][ld0]) and the actor head W4 ([ad][ld3]) are staged in LDS
+// behind the A tile, kHeadChunk outputs at a time, and shared by the workgroup's 4 waves.
+__device__ __forceinline__ void pro_actor_head_bwd(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = 2;
+  const int K0 = P.exi[0], ld0 = P.exi[1], ldw1 = P.exi[2], sd = P.exi[3], ad = P.exi[4];
+  const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
+  const float ma = P.exf[0];
+  float* w1s = smem + 32 * c.S;                 // [kHeadChunk][ld0]
+  float* w4s = w1s + kHeadChunk * ld0;          // [kHeadChunk][ld3]
+  float* ts = w4s + kHeadChunk * ld3;           // [32 rows][32] tanh outputs of the policy head
+  const int tid = c.wave * 64 + c.lane;
+  float g0[8];
+  if (P.norm) rv_load(g0, P.ex[3], ld0, c.lane);
+  const bool t0 = c.nt == 0;
+  // dU3 of the actor accumulates in this wave's 8 rows of the A tile (LDS)
+  {
+    float z[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) z[jj] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) lds_put_row(smem, c.S, c.wave * 8 + r, P.Kp, c.lane, z);
+  }
+  for (int o0 = 0; o0 < ad; o0 += kHeadChunk) {
+    const int oc = min(kHeadChunk, ad - o0);
+    __syncthreads();
+    for (int idx = tid; idx < oc * ld0; idx += 256) {
+      const int o = idx / ld0, n = idx - o * ld0;
+      w1s[idx] = n < K0 ? gld(P.ex[4] + ((size_t)n * ldw1 + sd + o0 + o)) : 0.f;   // W1[:, sd+o]
+    }
+    for (int idx = tid; idx < oc * ld3; idx += 256) {
+      const int o = idx / ld3, k = idx - o * ld3;
+      w4s[idx] = gld(P.ex[6] + ((size_t)(o0 + o) * ldw4 + k));
+    }
+    for (int idx = tid; idx < 32 * 32; idx += 256) ts[idx] = gld(P.ex[5] + ((size_t)c.m0 * 32 + idx));
+    __syncthreads();
+#pragma unroll 1
+    for (int r0 = 0; r0 < 8; r0 += RB) {
+      float gu0[RB][8], h0[RB][8], mn0[RB], rs0[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int grow = c.m0 + c.wave * 8 + r0 + r;
+        rv_load(gu0[r], P.ex[0] + (size_t)grow * ld0, ld0, c.lane);
+        rv_load(h0[r], P.ex[1] + (size_t)grow * ld0, ld0, c.lane);
+        mn0[r] = P.norm ? gld(P.ex[2] + grow) : 0.f;
+        rs0[r] = P.norm ? gld(P.ex[2] + (c.Bp + grow)) : 1.f;
+      }
+      ln_bwd_rows<RB>(gu0, h0, g0, mn0, rs0, K0, c.lane, P.norm);   // dZ0 of Q1
+      float gu3[RB][8];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) rv_load_lds(gu3[r], smem + (c.wave * 8 + r0 + r) * c.S, P.Kp, c.lane);
+#pragma unroll 1
+      for (int o = 0; o < oc; ++o) {
+        float w1o[8], w4o[8];
+        rv_load_lds(w1o, w1s + o * ld0, ld0, c.lane);
+        rv_load_lds(w4o, w4s + o * ld3, ld3, c.lane);
+        float sdot[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) sdot[r] = rv_pdot(gu0[r], w1o, K0, c.lane);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int row = c.wave * 8 + r0 + r, grow = c.m0 + row;
+          const float ga = wsum(sdot[r]);                               // dL/da_o
+          const float t = ts[row * 32 + o0 + o];
+          const float gz4 = grow < P.B ? (ga * ma) * (1.f - t * t) : 0.f;   // max_action*tanh bwd
+          if (t0 && c.lane == 0) gst(P.ex[10] + ((size_t)grow * 32 + o0 + o), gz4);
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) gu3[r][jj] += gz4 * w4o[jj];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * 8 + r0 + r, P.Kp, c.lane, gu3[r]);
+    }
+  }
+  float g3[8];
+  if (P.norm) rv_load(g3, P.ex[9], ld3, c.lane);
+#pragma unroll 1
+  for (int r0 = 0; r0 < 8; r0 += RB) {
+    float h3[RB][8], mn3[RB], rs3[RB], gz[RB][8];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int grow = c.m0 + c.wave * 8 + r0 + r;
+      rv_load(h3[r], P.ex[7] + (size_t)grow * ld3, ld3, c.lane);
+      mn3[r] = P.norm ? gld(P.ex[8] + grow) : 0.f;
+      rs3[r] = P.norm ? gld(P.ex[8] + (c.Bp + grow)) : 1.f;
+      rv_load_lds(gz[r], smem + (c.wave * 8 + r0 + r) * c.S, P.Kp, c.lane);
+      if (t0) rv_store(P.ex[11] + (size_t)grow * ld3, ld3, c.lane, gz[r]);
+    }
+    ln_bwd_rows<RB>(gz, h3, g3, mn3, rs3, K3, c.lane, P.norm);        // dZ3 of the actor
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = c.wave * 8 + r0 + r;
+      lds_put_row(smem, c.S, row, P.Kp, c.lane, gz[r]);
+      if (t0 && P.Aout) rv_store(P.Aout + (size_t)(c.m0 + row) * P.ldao, P.Kp, c.lane, gz[r]);
+    }
   }
 }
 
 // ================================================================== batch-row GEMM stage
-// Workgroup = 4 waves = one 32-row batch tile x (32*WN) output columns.
-//  * prologue: the workgroup's 32 A rows (full Kp) are read from HBM/L2 with float4
-//    loads, transformed row-wise (LayerNorm fwd, or LN bwd + ReLU bwd) by one wave
-//    per row and written to an LDS tile [32][S] (S == 4 mod 64: conflict-free b128
-//    fragment reads); n-tile 0 also stores the transformed rows for the dW kernel.
-//  * main loop: each wave owns a 32x32 output tile and a 1/WK slice of K; per 32-deep
-//    chunk a lane reads 16 A values (4x ds_read_b128) and 16 B values, and issues 16
-//    v_mfma_f32_32x32x2_f32 (lane half h supplies k = 16h + s of MFMA s).
-//  * WK > 1: the WK partial tiles are summed through LDS; epilogue bias/ReLU.
-template <int MODE, int WN>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmProb* __restrict__ probs, int nprob,
-                                                   int Bp, Counters* bump, int bump_actor) {
+// Workgroup = 4 waves = one 32-row batch tile x (32*WN) output columns; each wave owns a
+// 32x32 output tile and 1/WK of the K chunks (<= 4 chunks of 32 per wave).
+//  1. weight fragments of every chunk of the wave are requested first (64 VGPRs),
+//  2. the prologue builds the 32 A rows in LDS ([32][S], S == 4 mod 64 dwords: the
+//     ds_read_b128 fragment reads are bank-conflict free),
+//  3. per chunk a lane reads 16 A values (4x ds_read_b128) and issues 16
+//     v_mfma_f32_32x32x2_f32 (lane half h supplies k = 16h + s of MFMA s),
+//  4. WK > 1: the partial tiles are summed through LDS; bias / ReLU epilogue.
+constexpr int kMaxChunks = 4;
+
+template <int MODE>
+__device__ __forceinline__ void load_b(const GemmProb& P, float (&bv)[kMaxChunks][16], int cb, int nch,
+                                       int ncol, int h) {
+#pragma unroll
+  for (int cc = 0; cc < kMaxChunks; ++cc) {
+    const int ch = min(cb + cc, nch - 1);
+    const int kb = ch * 32 + 16 * h;
+    if (MODE == 0) {
+      const float* wp = P.W + (size_t)ncol * P.ldw + kb;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = gld4(wp + 4 * q);
+        bv[cc][4 * q + 0] = v.x; bv[cc][4 * q + 1] = v.y; bv[cc][4 * q + 2] = v.z; bv[cc][4 * q + 3] = v.w;
+      }
+    } else {
+      const float* wp = P.W + (size_t)kb * P.ldw + ncol;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) bv[cc][s] = gld(wp + (size_t)s * P.ldw);
+    }
+  }
+}
+
+template <int MODE, int WN, int PRO>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict__ probs, int nprob,
+                                                      int Bp, Counters* bump, int bump_actor) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
   constexpr int WK = 4 / WN;
+  constexpr bool kPrefetchB = (PRO == kProCopy || PRO == kProLN || PRO == kProLNBwd);
   const int b = blockIdx.x;
   if (bump && b == 0 && threadIdx.x == 0) {
     bump->total_it += 1;                       // TD3_featured.py:124
@@ -151,7 +651,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmProb* __restrict__ 
   int pi = 0;
   for (int i = 1; i < nprob; ++i)
     if (b >= probs[i].tile_begin) pi = i;
-  const GemmProb& P = probs[pi];
+  const GemmProb P = probs[pi];   // fields to registers before any store
   const int mtiles = Bp >> 5;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
@@ -160,170 +660,65 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmProb* __restrict__ 
   const int Kp = P.Kp;
   const int S = lds_stride(Kp);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool store_a = (nt == 0) && (P.Aout != nullptr);
-  const bool store_stats = (nt == 0) && (P.stats != nullptr);
-
-  // ---------------- prologue: 8 rows per wave, lane owns cols lane*4 + 256q
-  for (int rr = 0; rr < 8; ++rr) {
-    const int row = wave * 8 + rr, grow = m0 + row;
-    float4 x[2];
-    bool valid[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int c = lane * 4 + 256 * q;
-      valid[q] = c < Kp;
-      x[q] = valid[q] ? *reinterpret_cast<const float4*>(P.A + (size_t)grow * P.lda + c)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (P.pro == kProLN) {
-      const int K = P.Kreal;
-      float s = 0.f;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = lane * 4 + 256 * q;
-        if (c + 0 < K) s += x[q].x;
-        if (c + 1 < K) s += x[q].y;
-        if (c + 2 < K) s += x[q].z;
-        if (c + 3 < K) s += x[q].w;
-      }
-      const float mean = wave_sum(s) / (float)K;
-      float v = 0.f;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = lane * 4 + 256 * q;
-        float d;
-        if (c + 0 < K) { d = x[q].x - mean; v += d * d; }
-        if (c + 1 < K) { d = x[q].y - mean; v += d * d; }
-        if (c + 2 < K) { d = x[q].z - mean; v += d * d; }
-        if (c + 3 < K) { d = x[q].w - mean; v += d * d; }
-      }
-      const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
-      const float nb = -mean * rstd;
-      if (store_stats && lane == 0) {
-        P.stats[grow] = mean;
-        P.stats[Bp + grow] = rstd;
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (!valid[q]) continue;
-        const int c = lane * 4 + 256 * q;
-        const float4 g = *reinterpret_cast<const float4*>(P.lng + c);
-        const float4 bb = *reinterpret_cast<const float4*>(P.lnb + c);
-        x[q].x = (x[q].x * rstd + nb) * g.x + bb.x;
-        x[q].y = (x[q].y * rstd + nb) * g.y + bb.y;
-        x[q].z = (x[q].z * rstd + nb) * g.z + bb.z;
-        x[q].w = (x[q].w * rstd + nb) * g.w + bb.w;
-      }
-    } else if (P.pro == kProLNBwd || P.pro == kProReluBwd) {
-      float4 hh[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = lane * 4 + 256 * q;
-        hh[q] = valid[q] ? *reinterpret_cast<const float4*>(P.H + (size_t)grow * P.ldh + c)
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      if (P.pro == kProLNBwd) {
-        const int K = P.Kreal;
-        const float mean = P.stats[grow], rstd = P.stats[Bp + grow];
-        float4 xh[2], gx[2];
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int c = lane * 4 + 256 * q;
-          float4 g = valid[q] ? *reinterpret_cast<const float4*>(P.lng + c)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-          xh[q].x = (hh[q].x - mean) * rstd;
-          xh[q].y = (hh[q].y - mean) * rstd;
-          xh[q].z = (hh[q].z - mean) * rstd;
-          xh[q].w = (hh[q].w - mean) * rstd;
-          gx[q].x = x[q].x * g.x;
-          gx[q].y = x[q].y * g.y;
-          gx[q].z = x[q].z * g.z;
-          gx[q].w = x[q].w * g.w;
-          if (c + 0 < K) { s1 += gx[q].x; s2 += gx[q].x * xh[q].x; }
-          if (c + 1 < K) { s1 += gx[q].y; s2 += gx[q].y * xh[q].y; }
-          if (c + 2 < K) { s1 += gx[q].z; s2 += gx[q].z * xh[q].z; }
-          if (c + 3 < K) { s1 += gx[q].w; s2 += gx[q].w * xh[q].w; }
-        }
-        const float m1 = wave_sum(s1) / (float)K;
-        const float m2 = wave_sum(s2) / (float)K;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          x[q].x = hh[q].x > 0.f ? rstd * ((gx[q].x - m1) - xh[q].x * m2) : 0.f;
-          x[q].y = hh[q].y > 0.f ? rstd * ((gx[q].y - m1) - xh[q].y * m2) : 0.f;
-          x[q].z = hh[q].z > 0.f ? rstd * ((gx[q].z - m1) - xh[q].z * m2) : 0.f;
-          x[q].w = hh[q].w > 0.f ? rstd * ((gx[q].w - m1) - xh[q].w * m2) : 0.f;
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          x[q].x = hh[q].x > 0.f ? x[q].x : 0.f;
-          x[q].y = hh[q].y > 0.f ? x[q].y : 0.f;
-          x[q].z = hh[q].z > 0.f ? x[q].z : 0.f;
-          x[q].w = hh[q].w > 0.f ? x[q].w : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (!valid[q]) continue;
-      const int c = lane * 4 + 256 * q;
-      *reinterpret_cast<float4*>(smem + row * S + c) = x[q];
-      if (store_a) *reinterpret_cast<float4*>(P.Aout + (size_t)grow * P.ldao + c) = x[q];
-    }
-  }
-  __syncthreads();
-
-  // ---------------- MFMA main loop
+  const int i = lane & 31, h = lane >> 5;
   const int wn = wave % WN, wk = wave / WN;
   const int nch = Kp >> 5;
   const int cb = wk * nch / WK, ce = (wk + 1) * nch / WK;
-  const int i = lane & 31, h = lane >> 5;
   const int ncol0 = n0 + wn * 32;
   const bool active = ncol0 < P.Nout;
+  const int ncol = (active ? ncol0 : 0) + i;
+
+  float bv[kMaxChunks][16];
+  if constexpr (kPrefetchB) {
+    load_b<MODE>(P, bv, cb, nch, ncol, h);
+    __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
+  }
+
+  const Ctx c{m0, wave, lane, nt, Bp, S};
+  if constexpr (PRO == kProCopy) pro_copy<8>(P, smem, c);
+  else if constexpr (PRO == kProLN) pro_ln(P, smem, c);
+  else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
+  else if constexpr (PRO == kProTargetHead) pro_policy_head<true>(P, smem, c);
+  else if constexpr (PRO == kProPolicyHead) pro_policy_head<false>(P, smem, c);
+  else if constexpr (PRO == kProCriticLoss) pro_critic_loss(P, smem, c);
+  else if constexpr (PRO == kProActorLoss) pro_actor_loss(P, smem, c);
+  else if constexpr (PRO == kProActorHeadBwd) pro_actor_head_bwd(P, smem, c);
+
+  if constexpr (!kPrefetchB) load_b<MODE>(P, bv, cb, nch, ncol, h);
+  __syncthreads();
+
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   if (active) {
     const float* arow = smem + i * S + 16 * h;
-    const float* wbase = (MODE == 0) ? P.W + (size_t)(ncol0 + i) * P.ldw + 16 * h
-                                     : P.W + (size_t)(16 * h) * P.ldw + ncol0 + i;
-    for (int c = cb; c < ce; ++c) {
-      const int kb = c * 32;
-      float av[16], bv[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(arow + kb + 4 * q);
-        av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
-      }
-      if (MODE == 0) {
+    for (int cc = 0; cc < kMaxChunks; ++cc) {
+      if (cb + cc < ce) {
+        const int kb = (cb + cc) * 32;
+        float av[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(wbase + kb + 4 * q);
-          bv[4 * q + 0] = v.x; bv[4 * q + 1] = v.y; bv[4 * q + 2] = v.z; bv[4 * q + 3] = v.w;
+          const float4 v = *reinterpret_cast<const float4*>(arow + kb + 4 * q);
+          av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
         }
-      } else {
-        const float* wc = wbase + (size_t)kb * P.ldw;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) bv[s] = wc[(size_t)s * P.ldw];
+        for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[cc][s], acc);
       }
-#pragma unroll
-      for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[s], acc);
     }
   }
 
-  // ---------------- epilogue
   if constexpr (WK == 1) {
     if (active) {
       const int col = ncol0 + i;
-      const float bias = (MODE == 0 && P.bias) ? P.bias[col] : 0.f;
+      const float bias = (MODE == 0 && P.bias) ? gld(P.bias + (col)) : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = mfma_row(r, lane);
         float v = acc[r];
         if (MODE == 0 && P.bias) v = v + bias;
         if (P.relu) v = fmaxf(v, 0.f);
-        P.C[(size_t)(m0 + row) * P.ldc + col] = v;
+        gst(P.C + ((size_t)(m0 + row) * P.ldc + col), v);
       }
     }
   } else {
@@ -339,210 +734,70 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmProb* __restrict__ 
       float v = red[row * 33 + col];
 #pragma unroll
       for (int w = 1; w < 4; ++w) v = v + red[(w * 32 + row) * 33 + col];
-      if (MODE == 0 && P.bias) v = v + P.bias[n0 + col];
+      if (MODE == 0 && P.bias) v = v + gld(P.bias + (n0 + col));
       if (P.relu) v = fmaxf(v, 0.f);
-      P.C[(size_t)(m0 + row) * P.ldc + n0 + col] = v;
+      gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + col), v);
     }
   }
 }
 
-// ================================================================== heads (row-wise)
+// ================================================================== act / eval_q heads
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
-  const HeadProb& P = a.probs[blockIdx.y];
+  const HeadProb P = a.probs[blockIdx.y];
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.Bp) return;
-  float x[QR];
-  load_row<QR>(P.H3 + (size_t)row * P.ldh, P.K3, lane, x);
-  float u[QR];
+  float x[1][8], g[8], bb[8], mean[1], rstd[1];
+  const int ld = P.ldh;
+  rv_load(x[0], P.H3 + (size_t)row * ld, ld, lane);
   if (P.lng) {
-    float mean, rstd;
-    ln_stats<QR>(x, P.K3, lane, mean, rstd);
-    const float nb = -mean * rstd;
-#pragma unroll
-    for (int q = 0; q < QR; ++q) {
-      const int c = lane + 64 * q;
-      u[q] = c < P.K3 ? (x[q] * rstd + nb) * P.lng[c] + P.lnb[c] : 0.f;
-    }
+    rv_load(g, P.lng, ld, lane);
+    rv_load(bb, P.lnb, ld, lane);
+    ln_fwd_rows<1>(x, g, bb, P.K3, lane, mean, rstd);
     if (P.stats && lane == 0) {
-      P.stats[row] = mean;
-      P.stats[a.Bp + row] = rstd;
+      gst(P.stats + (row), mean[0]);
+      gst(P.stats + (a.Bp + row), rstd[0]);
     }
-  } else {
-#pragma unroll
-    for (int q = 0; q < QR; ++q) u[q] = x[q];
   }
-  if (P.U3) store_row<QR>(P.U3 + (size_t)row * P.ldu, P.ldu, lane, u);
+  if (P.U3) rv_store(P.U3 + (size_t)row * P.ldu, P.ldu, lane, x[0]);
   float zl = 0.f;
   for (int o = 0; o < P.nout; ++o) {
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < QR; ++q) {
-      const int c = lane + 64 * q;
-      if (c < P.K3) s += u[q] * P.W4[(size_t)o * P.ldw + c];
-    }
-    const float z = wave_sum(s) + P.b4[o];
+    float w[8];
+    rv_load(w, P.W4 + (size_t)o * P.ldw, P.ldw, lane);
+    const float z = wsum(rv_pdot(x[0], w, P.K3, lane)) + gld(P.b4 + (o));
     if (lane == o) zl = z;
   }
   if (lane >= P.nout) return;
   const int o = lane;
   const bool live = row < a.B;
-  if (P.mode == kHeadTargetAction) {
-    // TD3_featured.py:131-137 (noise = randn_like(action) * policy_noise, clamped)
-    float z;
-    if (a.gen_noise) {
-      float g4[4];
-      philox_normal4(a.seed, (uint64_t)a.ctr->total_it, kStreamNoise, (uint32_t)(row * 8 + (o >> 2)), g4);
-      z = g4[o & 3];
-      P.noise[(size_t)row * P.ldn + o] = z;
-    } else {
-      z = P.noise[(size_t)row * P.ldn + o];
-    }
-    float n = z * a.policy_noise;
-    n = fminf(fmaxf(n, -a.noise_clip), a.noise_clip);
-    float v = a.max_action * tanhf(zl) + n;
-    v = fminf(fmaxf(v, -a.max_action), a.max_action);
-    P.out[(size_t)row * P.ldo + P.out_col + o] = live ? v : 0.f;
-  } else if (P.mode == kHeadPolicy) {
-    const float th = tanhf(zl);                                  // TD3_featured.py:47-48
-    P.out[(size_t)row * P.ldo + P.out_col + o] = live ? a.max_action * th : 0.f;
-    P.tanh_out[(size_t)row * 32 + o] = th;
+  if (P.mode == kHeadPolicy) {
+    const float th = tanhf(zl);
+    gst(P.out + ((size_t)row * P.ldo + P.out_col + o), live ? a.max_action * th : 0.f);
+    if (P.tanh_out) gst(P.tanh_out + ((size_t)row * 32 + o), th);
   } else {
-    if (o == 0) P.out[row] = zl;
+    if (o == 0) gst(P.out + (row), zl);
   }
-}
-
-__global__ __launch_bounds__(256) void critic_loss_kernel(CriticLossArgs a, float two_over_b) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.Bp) return;
-  const bool live = row < a.B;
-  float tq[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    float x[QR];
-    load_row<QR>(a.TH3[j] + (size_t)row * a.ldh, a.K3, lane, x);
-    tq[j] = head_dot<QR>(x, a.K3, lane, a.norm ? a.Tlng[j] : nullptr, a.Tlnb[j], a.TW4[j], a.Tb4[j][0]);
-  }
-  const float tmin = fminf(tq[0], tq[1]);                             // :141
-  const float y = a.R[row] + (a.ND[row] * a.discount) * tmin;        // :142
-  if (lane == 0) a.Y[row] = y;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const float d = a.Qv[j][row] - y;
-    const float dq = live ? two_over_b * d : 0.f;                    // mse_loss backward
-    if (lane == 0) {
-      a.sqerr[j * a.Bp + row] = live ? d * d : 0.f;
-      a.GZ4[j][(size_t)row * a.ldgz4] = dq;
-    }
-    float gu[QR], h[QR], gz[QR];
-#pragma unroll
-    for (int q = 0; q < QR; ++q) {
-      const int c = lane + 64 * q;
-      gu[q] = c < a.K3 ? dq * a.W4[j][c] : 0.f;
-    }
-    load_row<QR>(a.H3[j] + (size_t)row * a.ldh, a.K3, lane, h);
-    float mean = 0.f, rstd = 1.f;
-    if (a.norm) {
-      mean = a.stats3[j][row];
-      rstd = a.stats3[j][a.Bp + row];
-    }
-    ln_relu_bwd<QR>(gu, h, a.lng3[j], a.K3, lane, mean, rstd, a.norm, gz);
-    store_row<QR>(a.GU3[j] + (size_t)row * a.ldh, a.ldh, lane, gu);
-    store_row<QR>(a.GZ3[j] + (size_t)row * a.ldh, a.ldh, lane, gz);
-  }
-}
-
-__global__ __launch_bounds__(256) void actor_loss_kernel(ActorLossArgs a, float neg_inv_b) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.Bp) return;
-  float h[QR];
-  load_row<QR>(a.H3 + (size_t)row * a.ldh, a.K3, lane, h);
-  float mean = 0.f, rstd = 1.f;
-  if (a.norm) ln_stats<QR>(h, a.K3, lane, mean, rstd);
-  const float q = head_dot<QR>(h, a.K3, lane, a.norm ? a.lng : nullptr, a.lnb, a.W4, a.b4[0]);
-  if (lane == 0) a.Qv[row] = q;
-  const float dq = row < a.B ? neg_inv_b : 0.f;                    // d(-mean)/dQ
-  float gu[QR], gz[QR];
-#pragma unroll
-  for (int qq = 0; qq < QR; ++qq) {
-    const int c = lane + 64 * qq;
-    gu[qq] = c < a.K3 ? dq * a.W4[c] : 0.f;
-  }
-  ln_relu_bwd<QR>(gu, h, a.lng, a.K3, lane, mean, rstd, a.norm, gz);
-  store_row<QR>(a.GZ3 + (size_t)row * a.ldh, a.ldh, lane, gz);
-}
-
-__global__ __launch_bounds__(256) void actor_head_bwd_kernel(ActorHeadBwdArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.Bp) return;
-  // Q1 layer-1: dZ1 = relu'(LN1_bwd(dU1))
-  float gu1[QR], h1[QR], gz1[QR];
-  load_row<QR>(a.GU1 + (size_t)row * a.ld1, a.K1, lane, gu1);
-  load_row<QR>(a.H1 + (size_t)row * a.ld1, a.K1, lane, h1);
-  float mean = 0.f, rstd = 1.f;
-  if (a.norm) {
-    mean = a.stats1[row];
-    rstd = a.stats1[a.Bp + row];
-  }
-  ln_relu_bwd<QR>(gu1, h1, a.lng1, a.K1, lane, mean, rstd, a.norm, gz1);
-  // dL/da = dZ1 * W1[:, sd:sd+ad]  (cat([state, action]) backward, TD3_featured.py:74)
-  float gz4 = 0.f;
-  for (int o = 0; o < a.ad; ++o) {
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < QR; ++q) {
-      const int c = lane + 64 * q;
-      if (c < a.K1) s += gz1[q] * a.W1[(size_t)c * a.ldw1 + a.sd + o];
-    }
-    const float ga = wave_sum(s);
-    if (lane == o) {
-      const float t = a.T[(size_t)row * a.ldt + o];
-      gz4 = row < a.B ? (ga * a.max_action) * (1.f - t * t) : 0.f;   // max_action*tanh backward
-    }
-  }
-  if (lane < a.ad) a.GZ4[(size_t)row * a.ldgz4 + lane] = gz4;
-  // actor head backward: dU3 = dZ4 * W4
-  float gu3[QR];
-#pragma unroll
-  for (int q = 0; q < QR; ++q) gu3[q] = 0.f;
-  for (int o = 0; o < a.ad; ++o) {
-    const float g = __shfl(gz4, o, 64);
-#pragma unroll
-    for (int q = 0; q < QR; ++q) {
-      const int c = lane + 64 * q;
-      if (c < a.K3) gu3[q] += g * a.W4[(size_t)o * a.ldw4 + c];
-    }
-  }
-  float h3[QR], gz3[QR];
-  load_row<QR>(a.H3 + (size_t)row * a.ld3, a.K3, lane, h3);
-  if (a.norm) {
-    mean = a.stats3[row];
-    rstd = a.stats3[a.Bp + row];
-  }
-  ln_relu_bwd<QR>(gu3, h3, a.lng3, a.K3, lane, mean, rstd, a.norm, gz3);
-  store_row<QR>(a.GU3 + (size_t)row * a.ld3, a.ld3, lane, gu3);
-  store_row<QR>(a.GZ3 + (size_t)row * a.ld3, a.ld3, lane, gz3);
 }
 
 __global__ __launch_bounds__(256) void lnbwd_rows_kernel(const LnBwdProb* __restrict__ probs, int Bp,
                                                          int norm) {
-  const LnBwdProb& P = probs[blockIdx.y];
+  constexpr int RB = 4;
+  const LnBwdProb P = probs[blockIdx.y];
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= Bp) return;
-  float gu[QR], h[QR], gz[QR];
-  load_row<QR>(P.GU + (size_t)row * P.ld, P.K, lane, gu);
-  load_row<QR>(P.H + (size_t)row * P.ld, P.K, lane, h);
-  float mean = 0.f, rstd = 1.f;
-  if (norm) {
-    mean = P.stats[row];
-    rstd = P.stats[Bp + row];
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RB;
+  if (row0 >= Bp) return;
+  float gu[RB][8], h[RB][8], g[8], mean[RB], rstd[RB];
+  if (norm) rv_load(g, P.lng, P.ld, lane);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    rv_load(gu[r], P.GU + (size_t)(row0 + r) * P.ld, P.ld, lane);
+    rv_load(h[r], P.H + (size_t)(row0 + r) * P.ld, P.ld, lane);
+    mean[r] = norm ? gld(P.stats + (row0 + r)) : 0.f;
+    rstd[r] = norm ? gld(P.stats + (Bp + row0 + r)) : 1.f;
   }
-  ln_relu_bwd<QR>(gu, h, P.lng, P.K, lane, mean, rstd, norm, gz);
-  store_row<QR>(P.GZ + (size_t)row * P.ld, P.ld, lane, gz);
+  ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.K, lane, norm);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rv_store(P.GZ + (size_t)(row0 + r) * P.ld, P.ld, lane, gu[r]);
 }
 
 // ================================================================== Adam / Polyak
@@ -571,106 +826,135 @@ __device__ __forceinline__ AdamK make_adam(const AdamArgs& a) {
 __device__ __forceinline__ void adam_elem(float* __restrict__ p, float* __restrict__ m,
                                           float* __restrict__ v, float g, const AdamK& k,
                                           float* __restrict__ t) {
-  float mm = *m, vv = *v, pp = *p;
+  float mm = gld(m), vv = gld(v), pp = gld(p);
   mm = __fmaf_rn(k.w1, g - mm, mm);
   vv = vv * k.b2;
   vv = vv + (k.c2 * g) * g;
   const float denom = sqrtf(vv) / k.bc2s + k.eps;
   pp = pp + (k.negss * mm) / denom;
-  *m = mm;
-  *v = vv;
-  *p = pp;
-  if (t) *t = k.tau * pp + k.omt * (*t);     // TD3_featured.py:167-171
+  gst(m, mm);
+  gst(v, vv);
+  gst(p, pp);
+  if (t) gst(t, k.tau * pp + k.omt * gld(t));     // TD3_featured.py:167-171
 }
 
 __device__ __forceinline__ void apply_grad(const DwArgs& a, const AdamK& k, int64_t idx, float g) {
   if (a.mode == kDwGrad) {
-    a.adam.G[idx] = g;
+    gst(a.adam.G + (idx), g);
   } else {
     adam_elem(a.adam.P + idx, a.adam.M + idx, a.adam.V + idx, g, k,
               a.mode == kDwAdamPolyak ? a.adam.T + idx : nullptr);
   }
 }
 
-// dW[n][k] = sum_r dZ[r][n] * U[r][k]  (32x32 tile per workgroup, rows split over 4 waves),
-// then bias / LN-affine reductions (k-tile 0 only) and the fused optimizer update.
-__global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
+__device__ __forceinline__ void dw_load_chunk(const DwProb& P, int rc, int h, int n0, int k0, int i,
+                                              float (&av)[16], float (&bv)[16]) {
+  const int rb = rc * 32 + 16 * h;
+  const float* gp = P.G + (size_t)rb * P.ldg + n0 + i;
+  const float* up = P.U + (size_t)rb * P.ldu + k0 + i;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    av[s] = gld(gp + (size_t)s * P.ldg);
+    bv[s] = gld(up + (size_t)s * P.ldu);
+  }
+}
+
+// Matrix tiles: dW[n][k] = sum_r dZ[r][n] * U[r][k] (32x32 per workgroup, rows split over the
+// 4 waves, operands of the next row chunk in flight while the current one is multiplied).
+// Vector tiles: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU over 32 columns.
+// Both end in the fused optimizer update of the elements they own.
+__global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a) {
   __shared__ float red[4 * 32 * 33];
-  __shared__ float vred[3][8][32];
   const int b = blockIdx.x;
   int pi = 0;
   for (int i = 1; i < a.nprob; ++i)
     if (b >= a.probs[i].tile_begin) pi = i;
-  const DwProb& P = a.probs[pi];
+  const DwProb P = a.probs[pi];
   const int t = b - P.tile_begin;
-  const int kt = t % P.ntk, nt = t / P.ntk;
-  const int n0 = nt * 32, k0 = kt * 32;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = lane & 31, h = lane >> 5;
-  const int nrc = a.Bp >> 5;
-  const int cb = wave * nrc / 4, ce = (wave + 1) * nrc / 4;
-  f32x16 acc;
+  const int nmat = (P.Np >> 5) * P.ntk;
+  const AdamK k = make_adam(a.adam);
+  if (t < nmat) {
+    const int kt = t % P.ntk, nt = t / P.ntk;
+    const int n0 = nt * 32, k0 = kt * 32;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = lane & 31, h = lane >> 5;
+    const int nrc = a.Bp >> 5;
+    const int cb = wave * nrc / 4, ce = (wave + 1) * nrc / 4;
+    f32x16 acc;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const float* gp = P.G + n0 + i;
-  const float* up = P.U + k0 + i;
-  for (int rc = cb; rc < ce; ++rc) {
-    const int rb = rc * 32 + 16 * h;
-    float av[16], bv[16];
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    float a0[16], b0[16], a1[16], b1[16];
+    if (cb < ce) dw_load_chunk(P, cb, h, n0, k0, i, a0, b0);
+    for (int rc = cb; rc < ce; rc += 2) {
+      if (rc + 1 < ce) dw_load_chunk(P, rc + 1, h, n0, k0, i, a1, b1);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      av[s] = gp[(size_t)(rb + s) * P.ldg];
-      bv[s] = up[(size_t)(rb + s) * P.ldu];
+      for (int s = 0; s < 16; ++s) acc = mfma32x32x2(a0[s], b0[s], acc);
+      if (rc + 1 >= ce) break;
+      if (rc + 2 < ce) dw_load_chunk(P, rc + 2, h, n0, k0, i, a0, b0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = mfma32x32x2(a1[s], b1[s], acc);
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[s], acc);
-  }
+    for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
+    __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
-
-  const bool vec = (kt == 0);
-  if (vec) {
-    // column sums over the batch: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU
-    const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
-    float sb = 0.f, sg = 0.f, sbeta = 0.f;
-    const bool ln = P.offg >= 0;
-    for (int r = rg; r < a.Bp; r += 8) {
-      sb += P.G[(size_t)r * P.ldg + n0 + c];
+    for (int q = 0; q < 4; ++q) {
+      const int e = threadIdx.x + 256 * q;
+      const int n = e >> 5, kk = e & 31;
+      float g = red[n * 33 + kk];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) g = g + red[(w * 32 + n) * 33 + kk];
+      apply_grad(a, k, P.offW + (int64_t)(n0 + n) * P.Kp + k0 + kk, g);
+    }
+    return;
+  }
+  // ---- vector tile
+  const int n0 = (t - nmat) * 32;
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const bool ln = P.offg >= 0;
+  float sb = 0.f, sg = 0.f, sbeta = 0.f;
+  for (int r0 = rg; r0 < a.Bp; r0 += 64) {
+    float gz[8], gu[8], hh[8], mu[8], rs[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = min(r0 + 8 * u, a.Bp - 1);      // clamped: loads stay unconditional
+      gz[u] = gld(P.G + ((size_t)r * P.ldg + n0 + c));
       if (ln) {
-        const float gu = P.GU[(size_t)r * P.ldgu + n0 + c];
-        const float xh = (P.H[(size_t)r * P.ldh + n0 + c] - P.stats[r]) * P.stats[a.Bp + r];
-        sg += gu * xh;
-        sbeta += gu;
+        gu[u] = gld(P.GU + ((size_t)r * P.ldgu + n0 + c));
+        hh[u] = gld(P.H + ((size_t)r * P.ldh + n0 + c));
+        mu[u] = gld(P.stats + r);
+        rs[u] = gld(P.stats + (a.Bp + r));
+      }
+      if (r0 + 8 * u >= a.Bp) {
+        gz[u] = 0.f;
+        gu[u] = 0.f;
       }
     }
-    vred[0][rg][c] = sb;
-    vred[1][rg][c] = sg;
-    vred[2][rg][c] = sbeta;
-  }
-  __syncthreads();
-  const AdamK k = make_adam(a.adam);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = threadIdx.x + 256 * q;
-    const int n = e >> 5, kk = e & 31;
-    float g = red[n * 33 + kk];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) g = g + red[(w * 32 + n) * 33 + kk];
-    apply_grad(a, k, P.offW + (int64_t)(n0 + n) * P.Kp + k0 + kk, g);
-  }
-  if (vec && threadIdx.x < 32) {
-    const int c = threadIdx.x;
-    float sb = 0.f, sg = 0.f, sbeta = 0.f;
-#pragma unroll
-    for (int rg = 0; rg < 8; ++rg) {
-      sb += vred[0][rg][c];
-      sg += vred[1][rg][c];
-      sbeta += vred[2][rg][c];
+    for (int u = 0; u < 8; ++u) {
+      sb += gz[u];
+      if (ln) {
+        sg += gu[u] * ((hh[u] - mu[u]) * rs[u]);
+        sbeta += gu[u];
+      }
     }
-    apply_grad(a, k, P.offb + n0 + c, sb);
-    if (P.offg >= 0) {
-      apply_grad(a, k, P.offg + n0 + c, sg);
-      apply_grad(a, k, P.offbeta + n0 + c, sbeta);
+  }
+  red[(0 * 8 + rg) * 32 + c] = sb;
+  red[(1 * 8 + rg) * 32 + c] = sg;
+  red[(2 * 8 + rg) * 32 + c] = sbeta;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      s0 += red[(0 * 8 + g) * 32 + c];
+      s1 += red[(1 * 8 + g) * 32 + c];
+      s2 += red[(2 * 8 + g) * 32 + c];
+    }
+    apply_grad(a, k, P.offb + n0 + c, s0);
+    if (ln) {
+      apply_grad(a, k, P.offg + n0 + c, s1);
+      apply_grad(a, k, P.offbeta + n0 + c, s2);
     }
   }
 }
@@ -678,7 +962,7 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, int polyak) {
   const AdamK k = make_adam(a);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float g = a.G[i] * k.gscale;
+    const float g = gld(a.G + (i)) * k.gscale;
     adam_elem(a.P + i, a.M + i, a.V + i, g, k, polyak ? a.T + i : nullptr);
   }
 }
@@ -686,28 +970,59 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, i
 __global__ __launch_bounds__(256) void polyak_flat_kernel(float* T, const float* P, int64_t n, float tau,
                                                           float omt) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    T[i] = tau * P[i] + omt * T[i];
+    gst(T + i, tau * gld(P + i) + omt * gld(T + i));
 }
 
 // ================================================================== launchers
-template <int MODE, int WN>
-static void gemm_launch_t(const GemmProb* d, int nprob, int nblocks, int Bp, int lds, Counters* bump,
-                          int bump_actor, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<MODE, WN>), dim3(nblocks), dim3(256), lds, s, d, nprob, Bp, bump,
-                     bump_actor);
+template <int MODE, int WN, int PRO>
+static void gl(const GemmProb* d, int nprob, int nblocks, int Bp, int lds, Counters* bump, int ba,
+               hipStream_t s) {
+  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(nblocks), dim3(256), lds, s, d, nprob, Bp, bump, ba);
 }
 
-int launch_gemm(int mode, int wn, const GemmProb* d, int nprob, int nblocks, int Bp, int lds,
+using GemmFn = void (*)(const GemmProb*, int, int, int, int, Counters*, int, hipStream_t);
+
+// Forward stages use Copy / LN / the two policy heads; input-grad stages use LN-bwd and the
+// three loss heads.  Only those combinations are instantiated.
+template <int WN>
+static GemmFn pick_fwd(int pro) {
+  switch (pro) {
+    case kProCopy: return gl<0, WN, kProCopy>;
+    case kProLN: return gl<0, WN, kProLN>;
+    case kProTargetHead: return gl<0, WN, kProTargetHead>;
+    case kProPolicyHead: return gl<0, WN, kProPolicyHead>;
+  }
+  return nullptr;
+}
+
+template <int WN>
+static GemmFn pick_bwd(int pro) {
+  switch (pro) {
+    case kProLNBwd: return gl<1, WN, kProLNBwd>;
+    case kProCriticLoss: return gl<1, WN, kProCriticLoss>;
+    case kProActorLoss: return gl<1, WN, kProActorLoss>;
+    case kProActorHeadBwd: return gl<1, WN, kProActorHeadBwd>;
+  }
+  return nullptr;
+}
+
+static GemmFn pick_gemm(int mode, int wn, int pro) {
+  if (mode == 0 && wn == 1) return pick_fwd<1>(pro);
+  if (mode == 0 && wn == 4) return pick_fwd<4>(pro);
+  if (mode == 1 && wn == 1) return pick_bwd<1>(pro);
+  if (mode == 1 && wn == 4) return pick_bwd<4>(pro);
+  return nullptr;
+}
+
+int launch_gemm(int mode, int wn, int pro, const GemmProb* d, int nprob, int nblocks, int Bp, int lds,
                 Counters* bump, int bump_actor, hipStream_t s) {
   if (nblocks <= 0) return 0;
-  if (mode == 0 && wn == 1) gemm_launch_t<0, 1>(d, nprob, nblocks, Bp, lds, bump, bump_actor, s);
-  else if (mode == 0 && wn == 4) gemm_launch_t<0, 4>(d, nprob, nblocks, Bp, lds, bump, bump_actor, s);
-  else if (mode == 1 && wn == 1) gemm_launch_t<1, 1>(d, nprob, nblocks, Bp, lds, bump, bump_actor, s);
-  else if (mode == 1 && wn == 4) gemm_launch_t<1, 4>(d, nprob, nblocks, Bp, lds, bump, bump_actor, s);
-  else {
-    set_error("launch_gemm: unsupported mode %d wn %d", mode, wn);
+  GemmFn f = pick_gemm(mode, wn, pro);
+  if (!f) {
+    set_error("launch_gemm: unsupported mode %d wn %d pro %d", mode, wn, pro);
     return -1;
   }
+  f(d, nprob, nblocks, Bp, lds, bump, bump_actor, s);
   TD3_HIP(hipGetLastError());
   return 0;
 }
@@ -718,28 +1033,8 @@ int launch_heads(const HeadArgs& a, int nprob, hipStream_t s) {
   return 0;
 }
 
-int launch_critic_loss(const CriticLossArgs& a, hipStream_t s) {
-  const float two_over_b = (float)(2.0 / (double)a.B);
-  hipLaunchKernelGGL(critic_loss_kernel, dim3(a.Bp / 4), dim3(256), 0, s, a, two_over_b);
-  TD3_HIP(hipGetLastError());
-  return 0;
-}
-
-int launch_actor_loss(const ActorLossArgs& a, hipStream_t s) {
-  const float neg_inv_b = (float)(-1.0) / (float)a.B;
-  hipLaunchKernelGGL(actor_loss_kernel, dim3(a.Bp / 4), dim3(256), 0, s, a, neg_inv_b);
-  TD3_HIP(hipGetLastError());
-  return 0;
-}
-
-int launch_actor_head_bwd(const ActorHeadBwdArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(actor_head_bwd_kernel, dim3(a.Bp / 4), dim3(256), 0, s, a);
-  TD3_HIP(hipGetLastError());
-  return 0;
-}
-
 int launch_lnbwd_rows(const LnBwdProb* d, int nprob, int Bp, int norm, hipStream_t s) {
-  hipLaunchKernelGGL(lnbwd_rows_kernel, dim3(Bp / 4, nprob), dim3(256), 0, s, d, Bp, norm);
+  hipLaunchKernelGGL(lnbwd_rows_kernel, dim3((Bp + 15) / 16, nprob), dim3(256), 0, s, d, Bp, norm);
   TD3_HIP(hipGetLastError());
   return 0;
 }
@@ -766,17 +1061,28 @@ int launch_polyak_flat(float* T, const float* P, int64_t n, float tau, hipStream
   return 0;
 }
 
-int kernels_init() {
+template <int WN>
+static int set_attr_all() {
   const int max_lds = 160 * 1024;
-  TD3_HIP(hipFuncSetAttribute((const void*)gemm_kernel<0, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
-  TD3_HIP(hipFuncSetAttribute((const void*)gemm_kernel<0, 4>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
-  TD3_HIP(hipFuncSetAttribute((const void*)gemm_kernel<1, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
-  TD3_HIP(hipFuncSetAttribute((const void*)gemm_kernel<1, 4>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
+#define TD3_ATTR(MODE, PRO)                                                                   \
+  TD3_HIP(hipFuncSetAttribute((const void*)gemm_kernel<MODE, WN, PRO>,                        \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, max_lds))
+  TD3_ATTR(0, kProCopy);
+  TD3_ATTR(0, kProLN);
+  TD3_ATTR(0, kProTargetHead);
+  TD3_ATTR(0, kProPolicyHead);
+  TD3_ATTR(1, kProLNBwd);
+  TD3_ATTR(1, kProCriticLoss);
+  TD3_ATTR(1, kProActorLoss);
+  TD3_ATTR(1, kProActorHeadBwd);
+#undef TD3_ATTR
   return 0;
+}
+
+int kernels_init() {
+  int rc = set_attr_all<1>();
+  if (!rc) rc = set_attr_all<4>();
+  return rc;
 }
 
 }  // namespace td3

@@ -123,6 +123,7 @@ struct Stage {
   std::string name;
   std::function<int(hipStream_t)> run;
   double flops = 0;
+  std::string kernel;   // HIP kernel function the stage launches (rocprof name)
 };
 
 struct Plan {
@@ -170,6 +171,7 @@ struct td3_handle {
   int nranks = 1, rank = 0;
   std::vector<Stage>* last_body = nullptr;
   std::vector<std::string> stage_names;
+  std::vector<std::string> stage_kernels;
 };
 
 namespace td3 {
@@ -213,32 +215,57 @@ static int gemm_lds_bytes(int Kp) {
 // store_u: keep the LN outputs U (input of the dW of the next layer);
 // stats: keep the LN row statistics (needed by any backward through this network).
 struct FwdItem { const NetL* net; const float* P; EvalB* e; bool store_u; bool stats; };
+struct BwdItem { const NetL* net; const float* P; EvalB* e; bool store_dz; };
 
-// Forward GEMM stages for layers 0..2 of several networks (one launch per layer).
+// Fills the prologue operands (ex / exi / exf) of problem `k` of a launch.
+using ProFill = std::function<void(GemmProb&, int)>;
+
+static int push_gemm_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
+                           std::vector<GemmProb>& probs, int mode, int wn, int pro, int Bp, int lds,
+                           int blocks, double flops, const std::string& name, Counters* bump,
+                           int bump_actor) {
+  void* d = nullptr;
+  TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
+  const int np = (int)probs.size();
+  const GemmProb* dp = (const GemmProb*)d;
+  char kname[64];
+  snprintf(kname, sizeof(kname), "td3::gemm_kernel<%d, %d, %d>", mode, wn, pro);
+  st.push_back({name,
+                [=](hipStream_t s) {
+                  return launch_gemm(mode, wn, pro, dp, np, blocks, Bp, lds, bump, bump_actor, s);
+                },
+                flops, kname});
+  return 0;
+}
+
+// Forward layers 0..2 of several networks (one launch per layer).  Layer 0 uses prologue
+// `pro0` (copy of the input rows, or a fused policy head filled by `fill0`).
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
-                          const std::vector<FwdItem>& items, int Bp, const char* tag,
-                          Counters* bump, int bump_actor) {
+                          const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
+                          Counters* bump, int bump_actor, int pro0 = kProCopy,
+                          const ProFill& fill0 = nullptr) {
   const bool norm = h->cfg.norm != 0;
   for (int l = 0; l < 3; ++l) {
     std::vector<GemmProb> probs;
     int maxKp = 0;
     for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Kp);
     const int wn = maxKp <= 128 ? 4 : 1;
-    int blocks = 0;
+    const int pro = l == 0 ? pro0 : (norm ? kProLN : kProCopy);
+    int blocks = 0, lds = 0;
     double flops = 0;
-    int lds = 0;
-    for (auto& it : items) {
+    for (size_t k = 0; k < items.size(); ++k) {
+      const FwdItem& it = items[k];
       const LinearL& L = it.net->lin[l];
       GemmProb p{};
+      p.norm = norm ? 1 : 0;
+      p.B = B;
       if (l == 0) {
         p.A = it.e->X;
         p.lda = it.e->ldx;
-        p.pro = kProNone;
       } else {
         p.A = it.e->H[l - 1];
         p.lda = it.net->lin[l - 1].Np;
         if (norm) {
-          p.pro = kProLN;
           p.lng = it.P + it.net->ln[l - 1].offg;
           p.lnb = it.P + it.net->ln[l - 1].offb;
           p.stats = it.stats ? it.e->stats[l - 1] : nullptr;
@@ -246,8 +273,6 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
             p.Aout = it.e->U[l - 1];
             p.ldao = L.Kp;
           }
-        } else {
-          p.pro = kProNone;
         }
       }
       p.Kreal = L.K;
@@ -261,28 +286,24 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.relu = 1;
       p.ntiles = (L.Np + 32 * wn - 1) / (32 * wn);
       p.tile_begin = blocks;
+      if (l == 0 && fill0) fill0(p, (int)k);
       blocks += (Bp / 32) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
       lds = std::max(lds, gemm_lds_bytes(L.Kp));
       probs.push_back(p);
     }
-    void* d = nullptr;
-    TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
-    const int np = (int)probs.size();
-    Counters* bp = (l == 0) ? bump : nullptr;
-    const GemmProb* dp = (const GemmProb*)d;
-    st.push_back({std::string(tag) + "_fwd" + std::to_string(l),
-                  [=](hipStream_t s) { return launch_gemm(0, wn, dp, np, blocks, Bp, lds, bp, bump_actor, s); },
-                  flops});
+    TD3_RC(push_gemm_stage(h, owned, st, probs, 0, wn, pro, Bp, lds, blocks, flops,
+                           std::string(tag) + "_fwd" + std::to_string(l), l == 0 ? bump : nullptr,
+                           bump_actor));
   }
   return 0;
 }
 
-struct BwdItem { const NetL* net; const float* P; EvalB* e; };
-
-// dU_{l-1} = dZ_l * W_l for l = 2, 1 (dZ_1 formed in the prologue from dU_1), then dZ_0 rows.
+// dU_1 = dZ_2 * W_2 (dZ_2 built by the fused head prologue `pro2`), dU_0 = dZ_1 * W_1
+// (dZ_1 = relu'(LN_bwd(dU_1)) in the prologue), then dZ_0 rows when needed.
 static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
-                          const std::vector<BwdItem>& items, int Bp, const char* tag, bool need_dz0) {
+                          const std::vector<BwdItem>& items, int Bp, int B, const char* tag,
+                          bool need_dz0, int pro2, const ProFill& fill2) {
   const bool norm = h->cfg.norm != 0;
   for (int l = 2; l >= 1; --l) {
     std::vector<GemmProb> probs;
@@ -291,23 +312,29 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     int maxKp = 0;
     for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Np);
     const int wn = maxKp <= 128 ? 4 : 1;
-    for (auto& it : items) {
+    for (size_t k = 0; k < items.size(); ++k) {
+      const BwdItem& it = items[k];
       const LinearL& L = it.net->lin[l];
       GemmProb p{};
+      p.norm = norm ? 1 : 0;
+      p.B = B;
       if (l == 2) {
-        p.A = it.e->GZ[2];
-        p.lda = L.Np;
-        p.pro = kProNone;
+        if (it.store_dz) {
+          p.Aout = it.e->GZ[2];
+          p.ldao = L.Np;
+        }
+        fill2(p, (int)k);
       } else {
         p.A = it.e->GU[1];
         p.lda = L.Np;
-        p.pro = norm ? kProLNBwd : kProReluBwd;
         p.H = it.e->H[1];
         p.ldh = L.Np;
         p.lng = it.P + it.net->ln[1].offg;
         p.stats = it.e->stats[1];
-        p.Aout = it.e->GZ[1];
-        p.ldao = L.Np;
+        if (it.store_dz) {
+          p.Aout = it.e->GZ[1];
+          p.ldao = L.Np;
+        }
       }
       p.Kreal = L.N;
       p.Kp = L.Np;
@@ -324,13 +351,12 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       lds = std::max(lds, gemm_lds_bytes(L.Np));
       probs.push_back(p);
     }
-    void* d = nullptr;
-    TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
-    const int np = (int)probs.size();
-    const GemmProb* dp = (const GemmProb*)d;
-    st.push_back({std::string(tag) + "_bwd" + std::to_string(l),
-                  [=](hipStream_t s) { return launch_gemm(1, wn, dp, np, blocks, Bp, lds, nullptr, 0, s); },
-                  flops});
+    if (l == 2 && pro2 == kProActorHeadBwd) {       // + LDS staging of the head weights
+      const GemmProb& q = probs[0];
+      lds = 4 * (32 * lds_stride(q.Kp) + kHeadChunk * (q.exi[1] + q.exi[6]) + 32 * 32);
+    }
+    TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, l == 2 ? pro2 : kProLNBwd, Bp, lds, blocks,
+                           flops, std::string(tag) + "_bwd" + std::to_string(l), nullptr, 0));
   }
   if (need_dz0) {
     std::vector<LnBwdProb> probs;
@@ -352,7 +378,8 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     const LnBwdProb* dp = (const LnBwdProb*)d;
     const int nrm = norm ? 1 : 0;
     st.push_back({std::string(tag) + "_lnbwd0",
-                  [=](hipStream_t s) { return launch_lnbwd_rows(dp, np, Bp, nrm, s); }, 0});
+                  [=](hipStream_t s) { return launch_lnbwd_rows(dp, np, Bp, nrm, s); }, 0,
+                  "td3::lnbwd_rows_kernel"});
   }
   return 0;
 }
@@ -392,7 +419,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       }
       p.ntk = L.Kp / 32;
       p.tile_begin = blocks;
-      blocks += (L.Np / 32) * p.ntk;
+      blocks += (L.Np / 32) * p.ntk + L.Np / 32;     // matrix tiles, then vector tiles
       flops += 2.0 * Bp * L.N * L.K;
       probs.push_back(p);
     }
@@ -418,7 +445,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.adam.grad_scale = 1.0f;
   const bool dp = h->comm != nullptr;
   a.mode = dp ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
-  st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops});
+  st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
+                "td3::dw_kernel"});
   if (dp) {
     ncclComm_t comm = h->comm;
     float* G = g.G;
@@ -432,12 +460,13 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                     }
                     return 0;
                   },
-                  0});
+                  0, "rccl"});
     AdamArgs aa = a.adam;
     aa.grad_scale = 1.0f / (float)h->nranks;
     const int pol = polyak ? 1 : 0;
     st.push_back({std::string(tag) + "_adam",
-                  [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s); }, 0});
+                  [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s); }, 0,
+                  "td3::adam_flat_kernel"});
   }
   return 0;
 }
@@ -522,170 +551,134 @@ static int build_step(td3_handle* h, int B) {
   const float* Ptq1 = h->critic.T;
   const float* Ptq2 = h->critic.T;
 
+  const float ma = h->cfg.max_action;
+  // fused policy-head operands (pro_policy_head in kernels.hip)
+  auto policy_head = [&](GemmProb& p, const float* Pp, EvalB& e, const float* state, int gen_noise) {
+    p.ex[0] = e.H[2];
+    p.ex[1] = const_cast<float*>(Pp + an.ln[2].offg);
+    p.ex[2] = const_cast<float*>(Pp + an.ln[2].offb);
+    p.ex[3] = const_cast<float*>(Pp + an.lin[3].offW);
+    p.ex[4] = const_cast<float*>(Pp + an.lin[3].offb);
+    p.ex[5] = P->noise;
+    p.ex[6] = const_cast<float*>(state);
+    p.exi[0] = an.lin[2].N;
+    p.exi[1] = an.lin[2].Np;
+    p.exi[2] = an.lin[3].Kp;
+    p.exi[3] = P->ld_s;
+    p.exi[4] = gen_noise;
+    p.exi[5] = ad;
+    p.exi[6] = sd;
+    p.exi[7] = ad;
+    p.exf[0] = ma;
+    p.exf[1] = (float)h->cfg.policy_noise;
+    p.exf[2] = (float)h->cfg.noise_clip;
+    p.seed = h->cfg.seed;
+    p.ctr = h->d_ctr;
+  };
+
   for (int actor_phase = 0; actor_phase < 2; ++actor_phase) {
     for (int inj = 0; inj < 2; ++inj) {
       std::vector<Stage>& st = P->body[actor_phase][inj];
-      // ---- forward of target actor, online twin (and online actor on policy steps)
+      // ---- forward of target actor (s'), online twin (s, a), online actor (s) on policy steps
       std::vector<FwdItem> f1 = {{&an, Pta, &P->TA, false, false}, {&q1, Pq1, &P->Q[0], true, true},
                                  {&q2, Pq2, &P->Q[1], true, true}};
       if (actor_phase) f1.push_back({&an, Pa, &P->A, true, true});
-      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, "F", h->d_ctr, actor_phase));
-      // ---- heads: next_action (target smoothing), Q1/Q2 values, pi(s)
-      {
-        std::vector<HeadProb> hp;
-        HeadProb p{};
-        auto base = [&](const NetL& n, const float* Pp, EvalB& e, int mode) {
-          HeadProb q{};
-          q.H3 = e.H[2];
-          q.ldh = n.lin[2].Np;
-          q.K3 = n.lin[2].N;
-          q.lng = norm ? Pp + n.ln[2].offg : nullptr;
-          q.lnb = norm ? Pp + n.ln[2].offb : nullptr;
-          q.W4 = Pp + n.lin[3].offW;
-          q.ldw = n.lin[3].Kp;
-          q.b4 = Pp + n.lin[3].offb;
-          q.nout = n.lin[3].N;
-          q.mode = mode;
-          return q;
-        };
-        p = base(an, Pta, P->TA, kHeadTargetAction);
-        p.out = P->X_S2A;
-        p.ldo = P->ld_sa;
-        p.out_col = sd;
-        p.noise = P->noise;
-        p.ldn = ad;
-        hp.push_back(p);
-        for (int j = 0; j < 2; ++j) {
-          const NetL& qn = j ? q2 : q1;
-          p = base(qn, j ? Pq2 : Pq1, P->Q[j], kHeadQ);
-          p.U3 = norm ? P->Q[j].U[2] : nullptr;
-          p.ldu = qn.lin[2].Np;
-          p.stats = P->Q[j].stats[2];
-          p.out = P->Q[j].Qv;
-          hp.push_back(p);
-        }
-        if (actor_phase) {
-          p = base(an, Pa, P->A, kHeadPolicy);
-          p.U3 = norm ? P->A.U[2] : nullptr;
-          p.ldu = an.lin[2].Np;
-          p.stats = P->A.stats[2];
-          p.out = P->X_SP;
-          p.ldo = P->ld_sa;
-          p.out_col = sd;
-          p.tanh_out = P->A.T;
-          hp.push_back(p);
-        }
-        void* d = nullptr;
-        TD3_RC(upload(h, P->tables, hp.data(), hp.size() * sizeof(HeadProb), &d));
-        HeadArgs a{};
-        a.probs = (const HeadProb*)d;
-        a.B = B;
-        a.Bp = Bp;
-        a.max_action = h->cfg.max_action;
-        a.policy_noise = (float)h->cfg.policy_noise;
-        a.noise_clip = (float)h->cfg.noise_clip;
-        a.ctr = h->d_ctr;
-        a.seed = h->cfg.seed;
-        a.gen_noise = inj ? 0 : 1;
-        const int np = (int)hp.size();
-        st.push_back({"heads", [=](hipStream_t s) { return launch_heads(a, np, s); }, 0});
-      }
-      // ---- target twin on (s', a')
+      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase));
+      // ---- target twin on (s', a'), a' = target smoothing fused into layer 0
       std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
-      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, "TF", nullptr, 0));
-      // ---- critic loss + LN3 backward of the twin
-      {
-        CriticLossArgs a{};
-        for (int j = 0; j < 2; ++j) {
-          const NetL& qn = j ? q2 : q1;
-          const float* Pt = j ? Ptq2 : Ptq1;
-          const float* Pp = j ? Pq2 : Pq1;
-          a.TH3[j] = P->TQ[j].H[2];
-          a.Tlng[j] = Pt + qn.ln[2].offg;
-          a.Tlnb[j] = Pt + qn.ln[2].offb;
-          a.TW4[j] = Pt + qn.lin[3].offW;
-          a.Tb4[j] = Pt + qn.lin[3].offb;
-          a.Qv[j] = P->Q[j].Qv;
-          a.H3[j] = P->Q[j].H[2];
-          a.stats3[j] = P->Q[j].stats[2];
-          a.lng3[j] = Pp + qn.ln[2].offg;
-          a.W4[j] = Pp + qn.lin[3].offW;
-          a.GZ4[j] = P->Q[j].GZ[3];
-          a.GU3[j] = P->Q[j].GU[2];
-          a.GZ3[j] = P->Q[j].GZ[2];
-        }
-        a.ldgz4 = 32;
-        a.ldh = q1.lin[2].Np;
-        a.K3 = q1.lin[2].N;
-        a.R = P->R;
-        a.ND = P->ND;
-        a.Y = P->Y;
-        a.sqerr = P->sqerr;
-        a.B = B;
-        a.Bp = Bp;
-        a.discount = (float)h->cfg.discount;
-        a.norm = norm ? 1 : 0;
-        st.push_back({"critic_loss", [=](hipStream_t s) { return launch_critic_loss(a, s); }, 0});
-      }
-      std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0]}, {&q2, Pq2, &P->Q[1]}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, "CB", true));
+      const int gen = inj ? 0 : 1;
+      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, kProTargetHead,
+                            [&, gen](GemmProb& p, int) { policy_head(p, Pta, P->TA, P->X_S2, gen); }));
+      // ---- critic loss (clipped double-Q target, mse) fused into the twin's layer-2 dX
+      std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0], true}, {&q2, Pq2, &P->Q[1], true}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true, kProCriticLoss,
+                            [&](GemmProb& p, int j) {
+                              const NetL& qt0 = q1;
+                              const NetL& qt1 = q2;
+                              const NetL& qj = j ? q2 : q1;
+                              p.ex[0] = P->TQ[0].H[2];
+                              p.ex[1] = P->TQ[1].H[2];
+                              p.ex[2] = P->Q[j].H[2];
+                              p.ex[3] = const_cast<float*>(Ptq1 + qt0.ln[2].offg);
+                              p.ex[4] = const_cast<float*>(Ptq2 + qt1.ln[2].offg);
+                              p.ex[5] = const_cast<float*>(Pq1 + qj.ln[2].offg);
+                              p.ex[6] = const_cast<float*>(Ptq1 + qt0.ln[2].offb);
+                              p.ex[7] = const_cast<float*>(Ptq2 + qt1.ln[2].offb);
+                              p.ex[8] = const_cast<float*>(Pq1 + qj.ln[2].offb);
+                              p.ex[9] = const_cast<float*>(Ptq1 + qt0.lin[3].offW);
+                              p.ex[10] = const_cast<float*>(Ptq2 + qt1.lin[3].offW);
+                              p.ex[11] = const_cast<float*>(Pq1 + qj.lin[3].offW);
+                              p.ex[12] = const_cast<float*>(Ptq1 + qt0.lin[3].offb);
+                              p.ex[13] = const_cast<float*>(Ptq2 + qt1.lin[3].offb);
+                              p.ex[14] = const_cast<float*>(Pq1 + qj.lin[3].offb);
+                              p.ex[15] = P->R;
+                              p.ex[16] = P->ND;
+                              p.ex[17] = P->Q[j].GZ[3];
+                              p.ex[18] = P->Q[j].GU[2];
+                              p.ex[19] = P->Q[j].U[2];
+                              p.ex[20] = P->Q[j].stats[2];
+                              p.ex[21] = P->Y;
+                              p.ex[22] = P->sqerr + (size_t)j * Bp;
+                              p.ex[23] = P->Q[j].Qv;
+                              p.exi[0] = qj.lin[2].N;
+                              p.exi[1] = qj.lin[2].Np;
+                              p.exi[2] = j;
+                              p.exf[0] = (float)h->cfg.discount;
+                              p.exf[1] = (float)(2.0 / (double)B);
+                            }));
       TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0));
       if (!actor_phase) continue;
       // ---------------- delayed policy update (TD3_featured.py:156-171)
+      // Q1(s, pi(s)) forward, pi fused into layer 0
       std::vector<FwdItem> f3 = {{&q1, Pq1, &P->AQ, false, true}};
-      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, "AF", nullptr, 0));
-      {
-        ActorLossArgs a{};
-        a.H3 = P->AQ.H[2];
-        a.ldh = q1.lin[2].Np;
-        a.K3 = q1.lin[2].N;
-        a.lng = Pq1 + q1.ln[2].offg;
-        a.lnb = Pq1 + q1.ln[2].offb;
-        a.W4 = Pq1 + q1.lin[3].offW;
-        a.b4 = Pq1 + q1.lin[3].offb;
-        a.Qv = P->AQ.Qv;
-        a.GZ3 = P->AQ.GZ[2];
-        a.B = B;
-        a.Bp = Bp;
-        a.norm = norm ? 1 : 0;
-        st.push_back({"actor_loss", [=](hipStream_t s) { return launch_actor_loss(a, s); }, 0});
-      }
-      std::vector<BwdItem> ab = {{&q1, Pq1, &P->AQ}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, "AQB", false));
-      {
-        ActorHeadBwdArgs a{};
-        a.GU1 = P->AQ.GU[0];
-        a.H1 = P->AQ.H[0];
-        a.stats1 = P->AQ.stats[0];
-        a.lng1 = Pq1 + q1.ln[0].offg;
-        a.ld1 = q1.lin[0].Np;
-        a.K1 = q1.lin[0].N;
-        a.W1 = Pq1 + q1.lin[0].offW;
-        a.ldw1 = q1.lin[0].Kp;
-        a.sd = sd;
-        a.ad = ad;
-        a.T = P->A.T;
-        a.ldt = 32;
-        a.max_action = h->cfg.max_action;
-        a.GZ4 = P->A.GZ[3];
-        a.ldgz4 = 32;
-        a.W4 = Pa + an.lin[3].offW;
-        a.ldw4 = an.lin[3].Kp;
-        a.H3 = P->A.H[2];
-        a.stats3 = P->A.stats[2];
-        a.lng3 = Pa + an.ln[2].offg;
-        a.ld3 = an.lin[2].Np;
-        a.K3 = an.lin[2].N;
-        a.GU3 = P->A.GU[2];
-        a.GZ3 = P->A.GZ[2];
-        a.B = B;
-        a.Bp = Bp;
-        a.norm = norm ? 1 : 0;
-        st.push_back({"actor_head_bwd", [=](hipStream_t s) { return launch_actor_head_bwd(a, s); }, 0});
-      }
-      std::vector<BwdItem> aa = {{&an, Pa, &P->A}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, aa, Bp, "AB", true));
-      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, aa, Bp, "A", true));
+      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0, kProPolicyHead,
+                            [&](GemmProb& p, int) {
+                              policy_head(p, Pa, P->A, P->X_S, 0);
+                              p.ex[7] = P->A.T;
+                              p.ex[8] = P->A.U[2];
+                              p.ex[9] = P->A.stats[2];
+                            }));
+      // -mean Q1 backward into Q1's layer 2, then dX through Q1 to its first layer
+      std::vector<BwdItem> aqb = {{&q1, Pq1, &P->AQ, false}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false, kProActorLoss,
+                            [&](GemmProb& p, int) {
+                              p.ex[0] = P->AQ.H[2];
+                              p.ex[1] = const_cast<float*>(Pq1 + q1.ln[2].offg);
+                              p.ex[2] = const_cast<float*>(Pq1 + q1.ln[2].offb);
+                              p.ex[3] = const_cast<float*>(Pq1 + q1.lin[3].offW);
+                              p.ex[4] = const_cast<float*>(Pq1 + q1.lin[3].offb);
+                              p.ex[5] = P->AQ.Qv;
+                              p.exi[0] = q1.lin[2].N;
+                              p.exi[1] = q1.lin[2].Np;
+                              p.exf[0] = (float)(-1.0) / (float)B;
+                            }));
+      // dQ1/da -> actor head backward fused into the actor's layer-2 dX
+      std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true, kProActorHeadBwd,
+                            [&](GemmProb& p, int) {
+                              p.ex[0] = P->AQ.GU[0];
+                              p.ex[1] = P->AQ.H[0];
+                              p.ex[2] = P->AQ.stats[0];
+                              p.ex[3] = const_cast<float*>(Pq1 + q1.ln[0].offg);
+                              p.ex[4] = const_cast<float*>(Pq1 + q1.lin[0].offW);
+                              p.ex[5] = P->A.T;
+                              p.ex[6] = const_cast<float*>(Pa + an.lin[3].offW);
+                              p.ex[7] = P->A.H[2];
+                              p.ex[8] = P->A.stats[2];
+                              p.ex[9] = const_cast<float*>(Pa + an.ln[2].offg);
+                              p.ex[10] = P->A.GZ[3];
+                              p.ex[11] = P->A.GU[2];
+                              p.exi[0] = q1.lin[0].N;
+                              p.exi[1] = q1.lin[0].Np;
+                              p.exi[2] = q1.lin[0].Kp;
+                              p.exi[3] = sd;
+                              p.exi[4] = ad;
+                              p.exi[5] = an.lin[2].N;
+                              p.exi[6] = an.lin[2].Np;
+                              p.exi[7] = an.lin[3].Kp;
+                              p.exf[0] = ma;
+                            }));
+      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true));
     }
   }
   if (h->plan) destroy_plan(h->plan.get());
@@ -859,7 +852,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
   };
   {
     std::vector<FwdItem> f = {{&an, h->actor.P, &A->A, false, false}};
-    TD3_RC(add_fwd_stages(h, A->tables, A->act, f, Bp, "act", nullptr, 0));
+    TD3_RC(add_fwd_stages(h, A->tables, A->act, f, Bp, Bp, "act", nullptr, 0));
     HeadProb p = head(an, h->actor.P, A->A, kHeadPolicy);
     p.out = A->X_SP;
     p.ldo = lds_sa;
@@ -877,7 +870,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
   {
     std::vector<FwdItem> f = {{&q1, h->critic.P, &A->Q[0], false, false},
                               {&q2, h->critic.P, &A->Q[1], false, false}};
-    TD3_RC(add_fwd_stages(h, A->tables, A->evalq, f, Bp, "evq", nullptr, 0));
+    TD3_RC(add_fwd_stages(h, A->tables, A->evalq, f, Bp, Bp, "evq", nullptr, 0));
     std::vector<HeadProb> hp;
     for (int j = 0; j < 2; ++j) {
       HeadProb p = head(j ? q2 : q1, h->critic.P, A->Q[j], kHeadQ);
@@ -1252,10 +1245,15 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   }
   TD3_HIP(hipStreamSynchronize(s));
   h->stage_names.clear();
+  h->stage_kernels.clear();
   h->stage_names.push_back("gather");
+  h->stage_kernels.push_back("td3::gather_kernel");
   for (int i = 0; i < n; ++i) {
     TD3_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
-    if (i) h->stage_names.push_back(st[i - 1].name);
+    if (i) {
+      h->stage_names.push_back(st[i - 1].name);
+      h->stage_kernels.push_back(st[i - 1].kernel);
+    }
   }
   for (auto& e : ev) hipEventDestroy(e);
   *n_stages = n;
@@ -1270,6 +1268,11 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
 const char* td3_stage_name(td3_handle* h, int i) {
   if (!h || i < 0 || i >= (int)h->stage_names.size()) return "";
   return h->stage_names[i].c_str();
+}
+
+const char* td3_stage_kernel(td3_handle* h, int i) {
+  if (!h || i < 0 || i >= (int)h->stage_kernels.size()) return "";
+  return h->stage_kernels[i].c_str();
 }
 
 double td3_stage_flops(td3_handle* h, int i) {
