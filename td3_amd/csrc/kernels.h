@@ -13,18 +13,21 @@ namespace td3 {
 // The prologue builds the workgroup's 32 A rows (full Kp) in LDS; its kind is a
 // template parameter of the kernel (one kind per launch):
 enum Pro : int {
-  kProCopy = 0,        // A rows as stored (network inputs)
+  kProCopy = 0,        // A rows as stored (network inputs, dZ rows from a row kernel)
   kProLN = 1,          // LayerNorm of the previous hidden layer (ReLU -> LN order)
   kProLNBwd = 2,       // dZ = relu'(LN_bwd(dU)) of the following layer
-  kProTargetHead = 3,  // [s' | a'] with a' = clamp(ma*tanh(head(LN3(H3_target_actor))) + eps)
-  kProPolicyHead = 4,  // [s | pi(s)],  pi = ma*tanh(head(LN3(H3_actor)))
-  kProCriticLoss = 5,  // dZ3 of Q_j from min(Q1',Q2') target, mse grad, head and LN3 backward
-  kProActorLoss = 6,   // dZ3 of Q1(s, pi(s)) from -mean(Q1), head and LN3 backward
-  kProActorHeadBwd = 7 // dZ3 of the actor from dQ1/da (Q1 LN1 bwd, W1 action cols, tanh bwd, head)
+};
+
+// Row kernels (one batch row per wave) between the GEMM stages; they reuse GemmProb's
+// ex / exi / exf operand slots (layout documented at each row function in kernels.hip).
+enum RowKind : int {
+  kRowPolicyHead = 0,    // a' = clamp(ma*tanh(head(LN3(H3))) + clip(eps)) or pi = ma*tanh(...)
+  kRowCriticLoss = 1,    // min(Q1',Q2') target, mse grad, Q head and LN3 backward of Q_j
+  kRowActorLoss = 2,     // -mean Q1(s, pi(s)): head and LN3 backward of Q1
+  kRowActorHeadBwd = 3   // dQ1/da (Q1 LN1 bwd, W1 action cols), tanh bwd, actor head + LN3 bwd
 };
 
 constexpr int kMaxEx = 24;
-constexpr int kHeadChunk = 16;   // actor-head outputs staged in LDS per chunk
 
 struct GemmProb {
   const float* A; int lda;        // batch rows of the A side (kProCopy / kProLN / kProLNBwd)
@@ -112,6 +115,7 @@ struct DwArgs {
 // ------------------------------------------------------------------ launchers (kernels.hip)
 int launch_gemm(int mode, int wn, int pro, const GemmProb* d_probs, int nprob, int nblocks, int Bp,
                 int lds_bytes, Counters* bump, int bump_actor, hipStream_t s);
+int launch_rows(int kind, const GemmProb* d_probs, int nprob, int Bp, hipStream_t s);
 int launch_heads(const HeadArgs& a, int nprob, hipStream_t s);
 int launch_lnbwd_rows(const LnBwdProb* d_probs, int nprob, int Bp, int norm, hipStream_t s);
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s);

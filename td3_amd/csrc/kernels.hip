@@ -257,130 +257,102 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
   }
 }
 
-// ---- fused heads of a policy network (target smoothing / pi(s)) -------------------------
-// ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=W4 ex[4]=b4 ex[5]=noise ex[6]=state rows
-// ex[7]=T out ex[8]=U3 out ex[9]=stats3 out
-// exi[0]=K3 exi[1]=ld3 exi[2]=ldw4 exi[3]=ld_state exi[4]=gen_noise exi[5]=ad exi[6]=sd exi[7]=ldn
+// ================================================================== row kernels
+// One batch row per wave (grid: Bp/4 x nprob, 256 threads): the head / loss work between the
+// GEMM stages.  Every operand of the row (and the head weights) is requested up front, the
+// reductions are DPP wave sums; a wave's serial chain is a single row.
+struct RowCtx {
+  int row, lane, Bp;
+};
+
+// ---- policy heads: target smoothing (TD3_featured.py:131-137) / pi(s) = ma*tanh (:47-48) --
+// ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=W4 ex[4]=b4 ex[5]=noise
+// out: ex[6]=critic input rows (action columns at sd..) ex[7]=T ex[8]=U3 ex[9]=stats3
+// exi[0]=K3 exi[1]=ld3 exi[2]=ldw4 exi[3]=ld_out exi[4]=gen_noise exi[5]=ad exi[6]=sd exi[7]=ldn
+// exi[8]=target (1: smoothing + clamp; 0: policy)
 // exf[0]=max_action exf[1]=policy_noise exf[2]=noise_clip
-template <bool TARGET>
-__device__ __forceinline__ void pro_policy_head(const GemmProb& P, float* smem, const Ctx& c) {
-  constexpr int RB = 4;
-  const int K3 = P.exi[0], ld3 = P.exi[1], ldw4 = P.exi[2], lds = P.exi[3];
+constexpr int kHeadRegs = 8;   // head outputs kept in registers (wider heads loop)
+
+__device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx& c) {
+  const int K3 = P.exi[0], ld3 = P.exi[1], ldw4 = P.exi[2];
   const int ad = P.exi[5], sd = P.exi[6];
+  const bool target = P.exi[8] != 0;
   const float ma = P.exf[0];
-  float g[8], bb[8];
+  float x[1][8], g[8], bb[8], mean[1], rstd[1];
+  float w4[kHeadRegs][8], b4v[kHeadRegs];
+  rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
   if (P.norm) {
     rv_load(g, P.ex[1], ld3, c.lane);
     rv_load(bb, P.ex[2], ld3, c.lane);
   }
-  constexpr int OM = 8;                 // head outputs kept in registers (ad <= 8 fast path)
-  float w4[OM][8], b4v[OM];
 #pragma unroll
-  for (int o = 0; o < OM; ++o) {
+  for (int o = 0; o < kHeadRegs; ++o) {
     const int oo = o < ad ? o : 0;
     rv_load(w4[o], P.ex[3] + (size_t)oo * ldw4, ldw4, c.lane);
     b4v[o] = gld(P.ex[4] + oo);
   }
-  const bool t0 = c.nt == 0;
+  float nz = 0.f;
+  if (target && !P.exi[4] && c.lane < ad) nz = gld(P.ex[5] + ((size_t)c.row * P.exi[7] + c.lane));
+  if (P.norm) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+  float mine = 0.f;                       // lane o keeps head output o
+  float part[kHeadRegs];
 #pragma unroll
-  for (int r0 = 0; r0 < 8; r0 += RB) {
-    float x[RB][8], st[RB][8], mean[RB], rstd[RB];
+  for (int o = 0; o < kHeadRegs; ++o) part[o] = rv_pdot(x[0], w4[o], K3, c.lane);
 #pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int grow = c.m0 + c.wave * 8 + r0 + r;
-      rv_load(x[r], P.ex[0] + (size_t)grow * ld3, ld3, c.lane);
-      rv_load(st[r], P.ex[6] + (size_t)grow * lds, lds, c.lane);
+  for (int o = 0; o < kHeadRegs; ++o)
+    if (o < ad) {
+      const float z = wsum(part[o]) + b4v[o];
+      if (c.lane == o) mine = z;
     }
-    if (P.norm) ln_fwd_rows<RB>(x, g, bb, K3, c.lane, mean, rstd);
-    // head Linear: z_o = u . W4[o] + b4[o]; lane o keeps output o
-    float mine[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) mine[r] = 0.f;
-#pragma unroll
-    for (int o = 0; o < OM; ++o) {
-      if (o < ad) {
-        float s[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) s[r] = rv_pdot(x[r], w4[o], K3, c.lane);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const float z = wsum(s[r]) + b4v[o];
-          if (c.lane == o) mine[r] = z;
-        }
-      }
-    }
-    for (int o = OM; o < ad; ++o) {                 // wide action spaces (ad > 8)
-      float w[8];
-      rv_load(w, P.ex[3] + (size_t)o * ldw4, ldw4, c.lane);
-      const float bo = gld(P.ex[4] + o);
-      float s[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) s[r] = rv_pdot(x[r], w, K3, c.lane);
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const float z = wsum(s[r]) + bo;
-        if (c.lane == o) mine[r] = z;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int row = c.wave * 8 + r0 + r, grow = c.m0 + row;
-      const bool live = grow < P.B;
-      float a = 0.f;
-      if (c.lane < ad) {
-        const int o = c.lane;
-        const float th = tanhf(mine[r]);
-        if (TARGET) {
-          float z;
-          if (P.exi[4]) {                                     // Philox N(0,1) (randn_like, :132)
-            float g4[4];
-            philox_normal4(P.seed, (uint64_t)P.ctr->total_it, kStreamNoise,
-                           (uint32_t)(grow * 8 + (o >> 2)), g4);
-            z = g4[o & 3];
-            if (t0) gst(P.ex[5] + ((size_t)grow * P.exi[7] + o), z);
-          } else {
-            z = gld(P.ex[5] + ((size_t)grow * P.exi[7] + o));
-          }
-          float n = z * P.exf[1];
-          n = fminf(fmaxf(n, -P.exf[2]), P.exf[2]);
-          float v = ma * th + n;                              // TD3_featured.py:135-137
-          a = fminf(fmaxf(v, -ma), ma);
-        } else {
-          a = ma * th;                                        // TD3_featured.py:47-48
-          if (t0) gst(P.ex[7] + ((size_t)grow * 32 + o), th);
-        }
-        if (!live) a = 0.f;
-      }
-      // A row = [state | action | 0]
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = rcol(c.lane, j);
-        const int o = col - sd;
-        const float av = __shfl(a, o >= 0 && o < 64 ? o : 0, 64);
-        v[j] = col < sd ? st[r][j] : (o < ad ? av : 0.f);
-      }
-      lds_put_row(smem, c.S, row, P.Kp, c.lane, v);
-      if (!TARGET && t0) {
-        if (P.norm) rv_store(P.ex[8] + (size_t)grow * ld3, ld3, c.lane, x[r]);
-        if (P.norm && c.lane == 0) {
-          gst(P.ex[9] + (grow), mean[r]);
-          gst(P.ex[9] + (c.Bp + grow), rstd[r]);
-        }
-      }
+  for (int o = kHeadRegs; o < ad; ++o) {
+    float w[8];
+    rv_load(w, P.ex[3] + (size_t)o * ldw4, ldw4, c.lane);
+    const float z = wsum(rv_pdot(x[0], w, K3, c.lane)) + gld(P.ex[4] + o);
+    if (c.lane == o) mine = z;
+  }
+  if (!target) {
+    if (P.norm) rv_store(P.ex[8] + (size_t)c.row * ld3, ld3, c.lane, x[0]);
+    if (P.norm && c.lane == 0) {
+      gst(P.ex[9] + c.row, mean[0]);
+      gst(P.ex[9] + (c.Bp + c.row), rstd[0]);
     }
   }
+  if (c.lane >= ad) return;
+  const int o = c.lane;
+  const bool live = c.row < P.B;
+  const float th = tanhf(mine);
+  float a;
+  if (target) {
+    float z = nz;
+    if (P.exi[4]) {                                          // Philox N(0,1) (randn_like, :132)
+      float g4[4];
+      philox_normal4(P.seed, (uint64_t)P.ctr->total_it, kStreamNoise, (uint32_t)(c.row * 8 + (o >> 2)), g4);
+      z = g4[o & 3];
+      gst(P.ex[5] + ((size_t)c.row * P.exi[7] + o), z);
+    }
+    float n = z * P.exf[1];
+    n = fminf(fmaxf(n, -P.exf[2]), P.exf[2]);
+    const float v = ma * th + n;
+    a = fminf(fmaxf(v, -ma), ma);
+  } else {
+    a = ma * th;
+    gst(P.ex[7] + ((size_t)c.row * 32 + o), th);
+  }
+  gst(P.ex[6] + ((size_t)c.row * P.exi[3] + sd + o), live ? a : 0.f);
 }
 
 // ---- clipped double-Q target + critic mse backward into LN3 of Q_j -----------------------
 // ex[0..2]=H3 of (target q1, target q2, online q_j)  ex[3..5]=gamma3  ex[6..8]=beta3
 // ex[9..11]=w4 (row 0)  ex[12..14]=b4  ex[15]=reward  ex[16]=not_done
-// out: ex[17]=dZ4_j (ld 32) ex[18]=dU3_j ex[19]=U3_j ex[20]=stats3_j ex[21]=y ex[22]=sqerr_j ex[23]=Q_j
+// out: ex[17]=dZ4_j (ld 32) ex[18]=dU3_j ex[19]=U3_j ex[20]=stats3_j ex[21]=y ex[22]=sqerr_j
+//      ex[23]=Q_j  Aout=dZ3_j
 // exi[0]=K3 exi[1]=ld3 exi[2]=j   exf[0]=discount exf[1]=2/B
-__device__ __forceinline__ void pro_critic_loss(const GemmProb& P, float* smem, const Ctx& c) {
-  constexpr int RB = 2;
+__device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx& c) {
   const int K3 = P.exi[0], ld3 = P.exi[1], j = P.exi[2];
-  float g[3][8], bb[3][8], w[3][8];
+  float x0[1][8], x1[1][8], xq[1][8], h[1][8], g[3][8], bb[3][8], w[3][8];
+  rv_load(x0[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
+  rv_load(x1[0], P.ex[1] + (size_t)c.row * ld3, ld3, c.lane);
+  rv_load(xq[0], P.ex[2] + (size_t)c.row * ld3, ld3, c.lane);
 #pragma unroll
   for (int n = 0; n < 3; ++n) {
     if (P.norm) {
@@ -389,217 +361,153 @@ __device__ __forceinline__ void pro_critic_loss(const GemmProb& P, float* smem, 
     }
     rv_load(w[n], P.ex[9 + n], ld3, c.lane);
   }
-  const float b40 = gld(P.ex[12] + (0)), b41 = gld(P.ex[13] + (0)), b4q = gld(P.ex[14] + (0));
-  const bool t0 = c.nt == 0;
+  const float b40 = gld(P.ex[12]), b41 = gld(P.ex[13]), b4q = gld(P.ex[14]);
+  const float rw = gld(P.ex[15] + c.row), nd = gld(P.ex[16] + c.row);
 #pragma unroll
-  for (int r0 = 0; r0 < 8; r0 += RB) {
-    float x0[RB][8], x1[RB][8], xq[RB][8], h[RB][8];
-    float m0[RB], s0[RB], m1[RB], s1[RB], mq[RB], sq[RB], rw[RB], nd[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int grow = c.m0 + c.wave * 8 + r0 + r;
-      rv_load(x0[r], P.ex[0] + (size_t)grow * ld3, ld3, c.lane);
-      rv_load(x1[r], P.ex[1] + (size_t)grow * ld3, ld3, c.lane);
-      rv_load(xq[r], P.ex[2] + (size_t)grow * ld3, ld3, c.lane);
-      rw[r] = gld(P.ex[15] + (grow));
-      nd[r] = gld(P.ex[16] + (grow));
-    }
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) h[r][jj] = xq[r][jj];
+  for (int jj = 0; jj < 8; ++jj) h[0][jj] = xq[0][jj];
+  float m0[1], s0[1], m1[1], s1[1], mq[1], sq[1];
+  if (P.norm) {
+    ln_fwd_rows<1>(x0, g[0], bb[0], K3, c.lane, m0, s0);
+    ln_fwd_rows<1>(x1, g[1], bb[1], K3, c.lane, m1, s1);
+    ln_fwd_rows<1>(xq, g[2], bb[2], K3, c.lane, mq, sq);
+  }
+  const float d0 = rv_pdot(x0[0], w[0], K3, c.lane);
+  const float d1 = rv_pdot(x1[0], w[1], K3, c.lane);
+  const float dq = rv_pdot(xq[0], w[2], K3, c.lane);
+  const float tq0 = wsum(d0) + b40, tq1 = wsum(d1) + b41, q = wsum(dq) + b4q;
+  const float y = rw + (nd * P.exf[0]) * fminf(tq0, tq1);                  // :141-142
+  const float d = q - y;
+  const bool live = c.row < P.B;
+  const float gq = live ? P.exf[1] * d : 0.f;                              // mse_loss bwd (:148)
+  if (c.lane == 0) {
+    gst(P.ex[17] + ((size_t)c.row * 32), gq);
+    gst(P.ex[23] + c.row, q);
+    gst(P.ex[22] + c.row, live ? d * d : 0.f);
+    if (j == 0) gst(P.ex[21] + c.row, y);
     if (P.norm) {
-      ln_fwd_rows<RB>(x0, g[0], bb[0], K3, c.lane, m0, s0);
-      ln_fwd_rows<RB>(x1, g[1], bb[1], K3, c.lane, m1, s1);
-      ln_fwd_rows<RB>(xq, g[2], bb[2], K3, c.lane, mq, sq);
-    }
-    float d0[RB], d1[RB], dq[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      d0[r] = rv_pdot(x0[r], w[0], K3, c.lane);
-      d1[r] = rv_pdot(x1[r], w[1], K3, c.lane);
-      dq[r] = rv_pdot(xq[r], w[2], K3, c.lane);
-    }
-    float gu[RB][8];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int row = c.wave * 8 + r0 + r, grow = c.m0 + row;
-      const float tq0 = wsum(d0[r]) + b40, tq1 = wsum(d1[r]) + b41, q = wsum(dq[r]) + b4q;
-      const float y = rw[r] + (nd[r] * P.exf[0]) * fminf(tq0, tq1);   // :141-142
-      const float d = q - y;
-      const bool live = grow < P.B;
-      const float gq = live ? P.exf[1] * d : 0.f;                   // mse_loss backward (:148)
-      if (t0 && c.lane == 0) {
-        gst(P.ex[17] + ((size_t)grow * 32), gq);
-        gst(P.ex[23] + grow, q);
-        gst(P.ex[22] + (grow), live ? d * d : 0.f);
-        if (j == 0) gst(P.ex[21] + (grow), y);
-        if (P.norm) {
-          gst(P.ex[20] + (grow), mq[r]);
-          gst(P.ex[20] + (c.Bp + grow), sq[r]);
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) gu[r][jj] = gq * w[2][jj];
-      if (t0) {
-        rv_store(P.ex[18] + (size_t)grow * ld3, ld3, c.lane, gu[r]);
-        if (P.norm) rv_store(P.ex[19] + (size_t)grow * ld3, ld3, c.lane, xq[r]);
-      }
-    }
-    ln_bwd_rows<RB>(gu, h, g[2], mq, sq, K3, c.lane, P.norm);
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int row = c.wave * 8 + r0 + r;
-      lds_put_row(smem, c.S, row, P.Kp, c.lane, gu[r]);
-      if (t0 && P.Aout) rv_store(P.Aout + (size_t)(c.m0 + row) * P.ldao, P.Kp, c.lane, gu[r]);
+      gst(P.ex[20] + c.row, mq[0]);
+      gst(P.ex[20] + (c.Bp + c.row), sq[0]);
     }
   }
+  float gu[1][8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) gu[0][jj] = gq * w[2][jj];
+  rv_store(P.ex[18] + (size_t)c.row * ld3, ld3, c.lane, gu[0]);
+  if (P.norm) rv_store(P.ex[19] + (size_t)c.row * ld3, ld3, c.lane, xq[0]);
+  ln_bwd_rows<1>(gu, h, g[2], mq, sq, K3, c.lane, P.norm);
+  rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
 }
 
-// ---- actor loss -mean Q1(s, pi(s)) backward into LN3 of Q1 --------------------------------
-// ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=w4 ex[4]=b4 out ex[5]=Q values
+// ---- actor loss -mean Q1(s, pi(s)) backward into LN3 of Q1 (:159) ------------------------
+// ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=w4 ex[4]=b4 out ex[5]=Q values, Aout=dZ3
 // exi[0]=K3 exi[1]=ld3   exf[0]=-1/B
-__device__ __forceinline__ void pro_actor_loss(const GemmProb& P, float* smem, const Ctx& c) {
-  constexpr int RB = 4;
+__device__ __forceinline__ void row_actor_loss(const GemmProb& P, const RowCtx& c) {
   const int K3 = P.exi[0], ld3 = P.exi[1];
-  float g[8], bb[8], w[8];
+  float x[1][8], h[1][8], g[8], bb[8], w[8], mean[1], rstd[1];
+  rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
   if (P.norm) {
     rv_load(g, P.ex[1], ld3, c.lane);
     rv_load(bb, P.ex[2], ld3, c.lane);
   }
   rv_load(w, P.ex[3], ld3, c.lane);
-  const float b4 = gld(P.ex[4] + (0));
+  const float b4 = gld(P.ex[4]);
 #pragma unroll
-  for (int r0 = 0; r0 < 8; r0 += RB) {
-    float x[RB][8], h[RB][8], mean[RB], rstd[RB];
+  for (int jj = 0; jj < 8; ++jj) h[0][jj] = x[0][jj];
+  if (P.norm) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+  const float q = wsum(rv_pdot(x[0], w, K3, c.lane)) + b4;
+  if (c.lane == 0) gst(P.ex[5] + c.row, q);
+  const float gq = c.row < P.B ? P.exf[0] : 0.f;
+  float gu[1][8];
 #pragma unroll
-    for (int r = 0; r < RB; ++r)
-      rv_load(x[r], P.ex[0] + (size_t)(c.m0 + c.wave * 8 + r0 + r) * ld3, ld3, c.lane);
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) h[r][jj] = x[r][jj];
-    if (P.norm) ln_fwd_rows<RB>(x, g, bb, K3, c.lane, mean, rstd);
-    float s[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) s[r] = rv_pdot(x[r], w, K3, c.lane);
-    float gu[RB][8];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int grow = c.m0 + c.wave * 8 + r0 + r;
-      const float q = wsum(s[r]) + b4;
-      if (c.nt == 0 && c.lane == 0) gst(P.ex[5] + (grow), q);
-      const float gq = grow < P.B ? P.exf[0] : 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) gu[r][jj] = gq * w[jj];
-    }
-    ln_bwd_rows<RB>(gu, h, g, mean, rstd, K3, c.lane, P.norm);
-#pragma unroll
-    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * 8 + r0 + r, P.Kp, c.lane, gu[r]);
-  }
+  for (int jj = 0; jj < 8; ++jj) gu[0][jj] = gq * w[jj];
+  ln_bwd_rows<1>(gu, h, g, mean, rstd, K3, c.lane, P.norm);
+  rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
 }
 
 // ---- dQ1/da through Q1's first layer, then the actor's head and LN3 backward -------------
 // ex[0]=dU0 of Q1(s,pi) ex[1]=H0 of Q1(s,pi) ex[2]=stats0 ex[3]=gamma0(q1) ex[4]=W1(q1)
 // ex[5]=T (tanh out) ex[6]=W4(actor) ex[7]=H3(actor) ex[8]=stats3(actor) ex[9]=gamma3(actor)
-// out: ex[10]=dZ4 actor (ld 32) ex[11]=dU3 actor
+// out: ex[10]=dZ4 actor (ld 32) ex[11]=dU3 actor  Aout=dZ3 actor
 // exi[0]=K0 exi[1]=ld0 exi[2]=ldw1 exi[3]=sd exi[4]=ad exi[5]=K3 exi[6]=ld3 exi[7]=ldw4
 // exf[0]=max_action
-// The action columns of W1 ([ad][ld0]) and the actor head W4 ([ad][ld3]) are staged in LDS
-// behind the A tile, kHeadChunk outputs at a time, and shared by the workgroup's 4 waves.
-__device__ __forceinline__ void pro_actor_head_bwd(const GemmProb& P, float* smem, const Ctx& c) {
-  constexpr int RB = 2;
+__device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowCtx& c) {
   const int K0 = P.exi[0], ld0 = P.exi[1], ldw1 = P.exi[2], sd = P.exi[3], ad = P.exi[4];
   const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
   const float ma = P.exf[0];
-  float* w1s = smem + 32 * c.S;                 // [kHeadChunk][ld0]
-  float* w4s = w1s + kHeadChunk * ld0;          // [kHeadChunk][ld3]
-  float* ts = w4s + kHeadChunk * ld3;           // [32 rows][32] tanh outputs of the policy head
-  const int tid = c.wave * 64 + c.lane;
-  float g0[8];
-  if (P.norm) rv_load(g0, P.ex[3], ld0, c.lane);
-  const bool t0 = c.nt == 0;
-  // dU3 of the actor accumulates in this wave's 8 rows of the A tile (LDS)
-  {
-    float z[8];
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) z[jj] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) lds_put_row(smem, c.S, c.wave * 8 + r, P.Kp, c.lane, z);
+  float gu0[1][8], h0[1][8], h3[1][8], g0[8], g3[8], mn0[1], rs0[1], mn3[1], rs3[1];
+  float w1[kHeadRegs][8], w4[kHeadRegs][8];
+  rv_load(gu0[0], P.ex[0] + (size_t)c.row * ld0, ld0, c.lane);
+  rv_load(h0[0], P.ex[1] + (size_t)c.row * ld0, ld0, c.lane);
+  rv_load(h3[0], P.ex[7] + (size_t)c.row * ld3, ld3, c.lane);
+  if (P.norm) {
+    rv_load(g0, P.ex[3], ld0, c.lane);
+    rv_load(g3, P.ex[9], ld3, c.lane);
+    mn0[0] = gld(P.ex[2] + c.row);
+    rs0[0] = gld(P.ex[2] + (c.Bp + c.row));
+    mn3[0] = gld(P.ex[8] + c.row);
+    rs3[0] = gld(P.ex[8] + (c.Bp + c.row));
+  } else {
+    mn0[0] = mn3[0] = 0.f;
+    rs0[0] = rs3[0] = 1.f;
   }
-  for (int o0 = 0; o0 < ad; o0 += kHeadChunk) {
-    const int oc = min(kHeadChunk, ad - o0);
-    __syncthreads();
-    for (int idx = tid; idx < oc * ld0; idx += 256) {
-      const int o = idx / ld0, n = idx - o * ld0;
-      w1s[idx] = n < K0 ? gld(P.ex[4] + ((size_t)n * ldw1 + sd + o0 + o)) : 0.f;   // W1[:, sd+o]
+  const float tl = c.lane < ad ? gld(P.ex[5] + ((size_t)c.row * 32 + c.lane)) : 0.f;
+#pragma unroll
+  for (int o = 0; o < kHeadRegs; ++o) {
+    const int oo = o < ad ? o : 0;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int n = rcol(c.lane, jj);
+      w1[o][jj] = gld(P.ex[4] + ((size_t)(n < K0 ? n : 0) * ldw1 + sd + oo));   // W1[:, sd+o]
     }
-    for (int idx = tid; idx < oc * ld3; idx += 256) {
-      const int o = idx / ld3, k = idx - o * ld3;
-      w4s[idx] = gld(P.ex[6] + ((size_t)(o0 + o) * ldw4 + k));
-    }
-    for (int idx = tid; idx < 32 * 32; idx += 256) ts[idx] = gld(P.ex[5] + ((size_t)c.m0 * 32 + idx));
-    __syncthreads();
-#pragma unroll 1
-    for (int r0 = 0; r0 < 8; r0 += RB) {
-      float gu0[RB][8], h0[RB][8], mn0[RB], rs0[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const int grow = c.m0 + c.wave * 8 + r0 + r;
-        rv_load(gu0[r], P.ex[0] + (size_t)grow * ld0, ld0, c.lane);
-        rv_load(h0[r], P.ex[1] + (size_t)grow * ld0, ld0, c.lane);
-        mn0[r] = P.norm ? gld(P.ex[2] + grow) : 0.f;
-        rs0[r] = P.norm ? gld(P.ex[2] + (c.Bp + grow)) : 1.f;
-      }
-      ln_bwd_rows<RB>(gu0, h0, g0, mn0, rs0, K0, c.lane, P.norm);   // dZ0 of Q1
-      float gu3[RB][8];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) rv_load_lds(gu3[r], smem + (c.wave * 8 + r0 + r) * c.S, P.Kp, c.lane);
-#pragma unroll 1
-      for (int o = 0; o < oc; ++o) {
-        float w1o[8], w4o[8];
-        rv_load_lds(w1o, w1s + o * ld0, ld0, c.lane);
-        rv_load_lds(w4o, w4s + o * ld3, ld3, c.lane);
-        float sdot[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) sdot[r] = rv_pdot(gu0[r], w1o, K0, c.lane);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const int row = c.wave * 8 + r0 + r, grow = c.m0 + row;
-          const float ga = wsum(sdot[r]);                               // dL/da_o
-          const float t = ts[row * 32 + o0 + o];
-          const float gz4 = grow < P.B ? (ga * ma) * (1.f - t * t) : 0.f;   // max_action*tanh bwd
-          if (t0 && c.lane == 0) gst(P.ex[10] + ((size_t)grow * 32 + o0 + o), gz4);
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) gu3[r][jj] += gz4 * w4o[jj];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * 8 + r0 + r, P.Kp, c.lane, gu3[r]);
-    }
+    rv_load(w4[o], P.ex[6] + (size_t)oo * ldw4, ldw4, c.lane);
   }
-  float g3[8];
-  if (P.norm) rv_load(g3, P.ex[9], ld3, c.lane);
-#pragma unroll 1
-  for (int r0 = 0; r0 < 8; r0 += RB) {
-    float h3[RB][8], mn3[RB], rs3[RB], gz[RB][8];
+  ln_bwd_rows<1>(gu0, h0, g0, mn0, rs0, K0, c.lane, P.norm);       // dZ0 of Q1 (pads -> 0)
+  const bool live = c.row < P.B;
+  float gu3[1][8];
 #pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int grow = c.m0 + c.wave * 8 + r0 + r;
-      rv_load(h3[r], P.ex[7] + (size_t)grow * ld3, ld3, c.lane);
-      mn3[r] = P.norm ? gld(P.ex[8] + grow) : 0.f;
-      rs3[r] = P.norm ? gld(P.ex[8] + (c.Bp + grow)) : 1.f;
-      rv_load_lds(gz[r], smem + (c.wave * 8 + r0 + r) * c.S, P.Kp, c.lane);
-      if (t0) rv_store(P.ex[11] + (size_t)grow * ld3, ld3, c.lane, gz[r]);
-    }
-    ln_bwd_rows<RB>(gz, h3, g3, mn3, rs3, K3, c.lane, P.norm);        // dZ3 of the actor
+  for (int jj = 0; jj < 8; ++jj) gu3[0][jj] = 0.f;
+  float part[kHeadRegs];
 #pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int row = c.wave * 8 + r0 + r;
-      lds_put_row(smem, c.S, row, P.Kp, c.lane, gz[r]);
-      if (t0 && P.Aout) rv_store(P.Aout + (size_t)(c.m0 + row) * P.ldao, P.Kp, c.lane, gz[r]);
+  for (int o = 0; o < kHeadRegs; ++o) part[o] = rv_pdot(gu0[0], w1[o], K0, c.lane);
+#pragma unroll
+  for (int o = 0; o < kHeadRegs; ++o)
+    if (o < ad) {
+      const float ga = wsum(part[o]);                                 // dL/da_o
+      const float t = __shfl(tl, o, 64);
+      const float gz4 = live ? (ga * ma) * (1.f - t * t) : 0.f;       // max_action*tanh bwd
+      if (c.lane == 0) gst(P.ex[10] + ((size_t)c.row * 32 + o), gz4);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4[o][jj];
     }
+  for (int o = kHeadRegs; o < ad; ++o) {                              // wide action spaces
+    float w1o[8], w4o[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int n = rcol(c.lane, jj);
+      w1o[jj] = n < K0 ? gld(P.ex[4] + ((size_t)n * ldw1 + sd + o)) : 0.f;
+    }
+    rv_load(w4o, P.ex[6] + (size_t)o * ldw4, ldw4, c.lane);
+    const float ga = wsum(rv_pdot(gu0[0], w1o, K0, c.lane));
+    const float t = gld(P.ex[5] + ((size_t)c.row * 32 + o));
+    const float gz4 = live ? (ga * ma) * (1.f - t * t) : 0.f;
+    if (c.lane == 0) gst(P.ex[10] + ((size_t)c.row * 32 + o), gz4);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4o[jj];
   }
+  rv_store(P.ex[11] + (size_t)c.row * ld3, ld3, c.lane, gu3[0]);
+  ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, P.norm);        // dZ3 of the actor
+  rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void row_kernel(const GemmProb* __restrict__ probs, int Bp) {
+  const GemmProb P = probs[blockIdx.y];
+  const RowCtx c{(int)(blockIdx.x * 4 + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
+  if (c.row >= Bp) return;
+  if constexpr (KIND == kRowPolicyHead) row_policy_head(P, c);
+  else if constexpr (KIND == kRowCriticLoss) row_critic_loss(P, c);
+  else if constexpr (KIND == kRowActorLoss) row_actor_loss(P, c);
+  else if constexpr (KIND == kRowActorHeadBwd) row_actor_head_bwd(P, c);
 }
 
 // ================================================================== batch-row GEMM stage
@@ -641,7 +549,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
   constexpr int WK = 4 / WN;
-  constexpr bool kPrefetchB = (PRO == kProCopy || PRO == kProLN || PRO == kProLNBwd);
+  constexpr bool kPrefetchB = true;
   const int b = blockIdx.x;
   if (bump && b == 0 && threadIdx.x == 0) {
     bump->total_it += 1;                       // TD3_featured.py:124
@@ -678,13 +586,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict
   if constexpr (PRO == kProCopy) pro_copy<8>(P, smem, c);
   else if constexpr (PRO == kProLN) pro_ln(P, smem, c);
   else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
-  else if constexpr (PRO == kProTargetHead) pro_policy_head<true>(P, smem, c);
-  else if constexpr (PRO == kProPolicyHead) pro_policy_head<false>(P, smem, c);
-  else if constexpr (PRO == kProCriticLoss) pro_critic_loss(P, smem, c);
-  else if constexpr (PRO == kProActorLoss) pro_actor_loss(P, smem, c);
-  else if constexpr (PRO == kProActorHeadBwd) pro_actor_head_bwd(P, smem, c);
-
-  if constexpr (!kPrefetchB) load_b<MODE>(P, bv, cb, nch, ncol, h);
   __syncthreads();
 
   f32x16 acc;
@@ -989,8 +890,6 @@ static GemmFn pick_fwd(int pro) {
   switch (pro) {
     case kProCopy: return gl<0, WN, kProCopy>;
     case kProLN: return gl<0, WN, kProLN>;
-    case kProTargetHead: return gl<0, WN, kProTargetHead>;
-    case kProPolicyHead: return gl<0, WN, kProPolicyHead>;
   }
   return nullptr;
 }
@@ -998,10 +897,8 @@ static GemmFn pick_fwd(int pro) {
 template <int WN>
 static GemmFn pick_bwd(int pro) {
   switch (pro) {
+    case kProCopy: return gl<1, WN, kProCopy>;
     case kProLNBwd: return gl<1, WN, kProLNBwd>;
-    case kProCriticLoss: return gl<1, WN, kProCriticLoss>;
-    case kProActorLoss: return gl<1, WN, kProActorLoss>;
-    case kProActorHeadBwd: return gl<1, WN, kProActorHeadBwd>;
   }
   return nullptr;
 }
@@ -1023,6 +920,23 @@ int launch_gemm(int mode, int wn, int pro, const GemmProb* d, int nprob, int nbl
     return -1;
   }
   f(d, nprob, nblocks, Bp, lds, bump, bump_actor, s);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_rows(int kind, const GemmProb* d, int nprob, int Bp, hipStream_t s) {
+  const dim3 grid(Bp / 4, nprob);
+  switch (kind) {
+    case kRowPolicyHead: hipLaunchKernelGGL(row_kernel<kRowPolicyHead>, grid, dim3(256), 0, s, d, Bp); break;
+    case kRowCriticLoss: hipLaunchKernelGGL(row_kernel<kRowCriticLoss>, grid, dim3(256), 0, s, d, Bp); break;
+    case kRowActorLoss: hipLaunchKernelGGL(row_kernel<kRowActorLoss>, grid, dim3(256), 0, s, d, Bp); break;
+    case kRowActorHeadBwd:
+      hipLaunchKernelGGL(row_kernel<kRowActorHeadBwd>, grid, dim3(256), 0, s, d, Bp);
+      break;
+    default:
+      set_error("launch_rows: unknown kind %d", kind);
+      return -1;
+  }
   TD3_HIP(hipGetLastError());
   return 0;
 }
@@ -1069,12 +983,8 @@ static int set_attr_all() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, max_lds))
   TD3_ATTR(0, kProCopy);
   TD3_ATTR(0, kProLN);
-  TD3_ATTR(0, kProTargetHead);
-  TD3_ATTR(0, kProPolicyHead);
+  TD3_ATTR(1, kProCopy);
   TD3_ATTR(1, kProLNBwd);
-  TD3_ATTR(1, kProCriticLoss);
-  TD3_ATTR(1, kProActorLoss);
-  TD3_ATTR(1, kProActorHeadBwd);
 #undef TD3_ATTR
   return 0;
 }

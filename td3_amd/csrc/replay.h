@@ -34,6 +34,7 @@ struct GatherSeg {
 };
 
 constexpr int kMaxSegs = 10;
+constexpr int kMaxRecord = 2048;   // floats per record the gather stages in LDS (2*sd+ad+2 <= 2048)
 struct GatherArgs {
   GatherSeg seg[kMaxSegs];
   int nseg;

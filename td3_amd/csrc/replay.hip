@@ -20,30 +20,32 @@ namespace td3 {
 // destination segment.  Rows B..Bp-1 are zero-filled so padded batch rows stay
 // finite and contribute nothing downstream.
 __global__ __launch_bounds__(256) void gather_kernel(GatherArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float rec_lds[4][kMaxRecord];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
   if (row >= a.Bp) return;
-  if (row >= a.B) {
-    for (int s = 0; s < a.nseg; ++s) {
-      const GatherSeg g = a.seg[s];
-      for (int c = lane; c < g.len; c += 64) g.dst[(size_t)row * g.ld + g.col + c] = 0.f;
+  float* lr = rec_lds[wave];
+  if (row < a.B) {
+    int64_t idx;
+    if (a.inject_idx) {
+      idx = a.inject_idx[row];
+    } else {
+      const uint64_t step = a.ctr ? (uint64_t)(a.ctr->total_it + 1) : a.step;
+      idx = (int64_t)philox_index(a.seed, step, (uint32_t)row, (uint64_t)*a.d_size);
     }
-    return;
-  }
-  int64_t idx;
-  if (a.inject_idx) {
-    idx = a.inject_idx[row];
+    if (a.idx_out && lane == 0) a.idx_out[row] = idx;
+    // the whole record first (every load in flight), then the scatter into the segments
+    const float4* src = reinterpret_cast<const float4*>(a.data + (size_t)idx * a.rec);
+    for (int c = lane; c < (a.rec >> 2); c += 64) reinterpret_cast<float4*>(lr)[c] = src[c];
   } else {
-    const uint64_t step = a.ctr ? (uint64_t)(a.ctr->total_it + 1) : a.step;
-    const int64_t n = *a.d_size;
-    idx = (int64_t)philox_index(a.seed, step, (uint32_t)row, (uint64_t)n);
+    for (int c = lane; c < a.rec; c += 64) lr[c] = 0.f;          // padded rows stay zero
   }
-  if (a.idx_out && lane == 0) a.idx_out[row] = idx;
-  const float* src = a.data + (size_t)idx * a.rec;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   for (int s = 0; s < a.nseg; ++s) {
     const GatherSeg g = a.seg[s];
     float* d = g.dst + (size_t)row * g.ld + g.col;
-    for (int c = lane; c < g.len; c += 64) d[c] = src[g.src + c];
+    for (int c = lane; c < g.len; c += 64) d[c] = row < a.B ? lr[g.src + c] : 0.f;
   }
 }
 
@@ -102,6 +104,7 @@ int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint6
               rb_handle** out) {
   TD3_ARG(out != nullptr, "out is null");
   TD3_ARG(state_dim > 0 && action_dim > 0, "dims must be positive");
+  TD3_ARG(pad4(2 * state_dim + action_dim + 2) <= kMaxRecord, "record too wide");
   TD3_ARG(max_size > 0, "max_size must be positive");
   TD3_HIP(hipSetDevice(device));
   Ring* r = new Ring();

@@ -217,9 +217,6 @@ static int gemm_lds_bytes(int Kp) {
 struct FwdItem { const NetL* net; const float* P; EvalB* e; bool store_u; bool stats; };
 struct BwdItem { const NetL* net; const float* P; EvalB* e; bool store_dz; };
 
-// Fills the prologue operands (ex / exi / exf) of problem `k` of a launch.
-using ProFill = std::function<void(GemmProb&, int)>;
-
 static int push_gemm_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                            std::vector<GemmProb>& probs, int mode, int wn, int pro, int Bp, int lds,
                            int blocks, double flops, const std::string& name, Counters* bump,
@@ -238,19 +235,30 @@ static int push_gemm_stage(td3_handle* h, std::vector<void*>& owned, std::vector
   return 0;
 }
 
-// Forward layers 0..2 of several networks (one launch per layer).  Layer 0 uses prologue
-// `pro0` (copy of the input rows, or a fused policy head filled by `fill0`).
+static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
+                          std::vector<GemmProb>& probs, int kind, int Bp, const std::string& name) {
+  void* d = nullptr;
+  TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
+  const int np = (int)probs.size();
+  const GemmProb* dp = (const GemmProb*)d;
+  char kname[64];
+  snprintf(kname, sizeof(kname), "td3::row_kernel<%d>", kind);
+  st.push_back({name, [=](hipStream_t s) { return launch_rows(kind, dp, np, Bp, s); }, 0, kname});
+  return 0;
+}
+
+// Forward layers 0..2 of several networks (one launch per layer); layer 0 copies the
+// network input rows, layers 1 and 2 apply the previous layer's LayerNorm in the prologue.
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
-                          Counters* bump, int bump_actor, int pro0 = kProCopy,
-                          const ProFill& fill0 = nullptr) {
+                          Counters* bump, int bump_actor) {
   const bool norm = h->cfg.norm != 0;
   for (int l = 0; l < 3; ++l) {
     std::vector<GemmProb> probs;
     int maxKp = 0;
     for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Kp);
     const int wn = maxKp <= 128 ? 4 : 1;
-    const int pro = l == 0 ? pro0 : (norm ? kProLN : kProCopy);
+    const int pro = l == 0 ? kProCopy : (norm ? kProLN : kProCopy);
     int blocks = 0, lds = 0;
     double flops = 0;
     for (size_t k = 0; k < items.size(); ++k) {
@@ -286,7 +294,6 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.relu = 1;
       p.ntiles = (L.Np + 32 * wn - 1) / (32 * wn);
       p.tile_begin = blocks;
-      if (l == 0 && fill0) fill0(p, (int)k);
       blocks += (Bp / 32) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
       lds = std::max(lds, gemm_lds_bytes(L.Kp));
@@ -303,7 +310,7 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 // (dZ_1 = relu'(LN_bwd(dU_1)) in the prologue), then dZ_0 rows when needed.
 static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<BwdItem>& items, int Bp, int B, const char* tag,
-                          bool need_dz0, int pro2, const ProFill& fill2) {
+                          bool need_dz0) {
   const bool norm = h->cfg.norm != 0;
   for (int l = 2; l >= 1; --l) {
     std::vector<GemmProb> probs;
@@ -318,12 +325,9 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       GemmProb p{};
       p.norm = norm ? 1 : 0;
       p.B = B;
-      if (l == 2) {
-        if (it.store_dz) {
-          p.Aout = it.e->GZ[2];
-          p.ldao = L.Np;
-        }
-        fill2(p, (int)k);
+      if (l == 2) {                       // dZ2 rows come from the loss / head row kernel
+        p.A = it.e->GZ[2];
+        p.lda = L.Np;
       } else {
         p.A = it.e->GU[1];
         p.lda = L.Np;
@@ -351,11 +355,7 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       lds = std::max(lds, gemm_lds_bytes(L.Np));
       probs.push_back(p);
     }
-    if (l == 2 && pro2 == kProActorHeadBwd) {       // + LDS staging of the head weights
-      const GemmProb& q = probs[0];
-      lds = 4 * (32 * lds_stride(q.Kp) + kHeadChunk * (q.exi[1] + q.exi[6]) + 32 * 32);
-    }
-    TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, l == 2 ? pro2 : kProLNBwd, Bp, lds, blocks,
+    TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, l == 2 ? kProCopy : kProLNBwd, Bp, lds, blocks,
                            flops, std::string(tag) + "_bwd" + std::to_string(l), nullptr, 0));
   }
   if (need_dz0) {
@@ -552,28 +552,36 @@ static int build_step(td3_handle* h, int B) {
   const float* Ptq2 = h->critic.T;
 
   const float ma = h->cfg.max_action;
-  // fused policy-head operands (pro_policy_head in kernels.hip)
-  auto policy_head = [&](GemmProb& p, const float* Pp, EvalB& e, const float* state, int gen_noise) {
+  // policy-head row operands (row_policy_head in kernels.hip)
+  auto policy_head = [&](const float* Pp, EvalB& e, float* out, int target, int gen_noise) {
+    GemmProb p{};
+    p.norm = norm ? 1 : 0;
+    p.B = B;
     p.ex[0] = e.H[2];
     p.ex[1] = const_cast<float*>(Pp + an.ln[2].offg);
     p.ex[2] = const_cast<float*>(Pp + an.ln[2].offb);
     p.ex[3] = const_cast<float*>(Pp + an.lin[3].offW);
     p.ex[4] = const_cast<float*>(Pp + an.lin[3].offb);
     p.ex[5] = P->noise;
-    p.ex[6] = const_cast<float*>(state);
+    p.ex[6] = out;
+    p.ex[7] = e.T;
+    p.ex[8] = e.U[2];
+    p.ex[9] = e.stats[2];
     p.exi[0] = an.lin[2].N;
     p.exi[1] = an.lin[2].Np;
     p.exi[2] = an.lin[3].Kp;
-    p.exi[3] = P->ld_s;
+    p.exi[3] = P->ld_sa;
     p.exi[4] = gen_noise;
     p.exi[5] = ad;
     p.exi[6] = sd;
     p.exi[7] = ad;
+    p.exi[8] = target;
     p.exf[0] = ma;
     p.exf[1] = (float)h->cfg.policy_noise;
     p.exf[2] = (float)h->cfg.noise_clip;
     p.seed = h->cfg.seed;
     p.ctr = h->d_ctr;
+    return p;
   };
 
   for (int actor_phase = 0; actor_phase < 2; ++actor_phase) {
@@ -584,100 +592,117 @@ static int build_step(td3_handle* h, int B) {
                                  {&q2, Pq2, &P->Q[1], true, true}};
       if (actor_phase) f1.push_back({&an, Pa, &P->A, true, true});
       TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase));
-      // ---- target twin on (s', a'), a' = target smoothing fused into layer 0
+      // ---- heads: a' = target smoothing into X_S2A (:131-137); pi(s) into X_SP (:159)
+      {
+        std::vector<GemmProb> hp = {policy_head(Pta, P->TA, P->X_S2A, 1, inj ? 0 : 1)};
+        if (actor_phase) hp.push_back(policy_head(Pa, P->A, P->X_SP, 0, 0));
+        TD3_RC(push_row_stage(h, P->tables, st, hp, kRowPolicyHead, Bp, "heads"));
+      }
+      // ---- target twin on (s', a')
       std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
-      const int gen = inj ? 0 : 1;
-      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, kProTargetHead,
-                            [&, gen](GemmProb& p, int) { policy_head(p, Pta, P->TA, P->X_S2, gen); }));
-      // ---- critic loss (clipped double-Q target, mse) fused into the twin's layer-2 dX
+      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0));
+      // ---- critic loss (clipped double-Q target, mse) and LN3 backward of the twin
+      {
+        std::vector<GemmProb> cl;
+        for (int j = 0; j < 2; ++j) {
+          const NetL& qj = j ? q2 : q1;
+          GemmProb p{};
+          p.norm = norm ? 1 : 0;
+          p.B = B;
+          p.ex[0] = P->TQ[0].H[2];
+          p.ex[1] = P->TQ[1].H[2];
+          p.ex[2] = P->Q[j].H[2];
+          p.ex[3] = const_cast<float*>(Ptq1 + q1.ln[2].offg);
+          p.ex[4] = const_cast<float*>(Ptq2 + q2.ln[2].offg);
+          p.ex[5] = const_cast<float*>(Pq1 + qj.ln[2].offg);
+          p.ex[6] = const_cast<float*>(Ptq1 + q1.ln[2].offb);
+          p.ex[7] = const_cast<float*>(Ptq2 + q2.ln[2].offb);
+          p.ex[8] = const_cast<float*>(Pq1 + qj.ln[2].offb);
+          p.ex[9] = const_cast<float*>(Ptq1 + q1.lin[3].offW);
+          p.ex[10] = const_cast<float*>(Ptq2 + q2.lin[3].offW);
+          p.ex[11] = const_cast<float*>(Pq1 + qj.lin[3].offW);
+          p.ex[12] = const_cast<float*>(Ptq1 + q1.lin[3].offb);
+          p.ex[13] = const_cast<float*>(Ptq2 + q2.lin[3].offb);
+          p.ex[14] = const_cast<float*>(Pq1 + qj.lin[3].offb);
+          p.ex[15] = P->R;
+          p.ex[16] = P->ND;
+          p.ex[17] = P->Q[j].GZ[3];
+          p.ex[18] = P->Q[j].GU[2];
+          p.ex[19] = P->Q[j].U[2];
+          p.ex[20] = P->Q[j].stats[2];
+          p.ex[21] = P->Y;
+          p.ex[22] = P->sqerr + (size_t)j * Bp;
+          p.ex[23] = P->Q[j].Qv;
+          p.Aout = P->Q[j].GZ[2];
+          p.ldao = qj.lin[2].Np;
+          p.exi[0] = qj.lin[2].N;
+          p.exi[1] = qj.lin[2].Np;
+          p.exi[2] = j;
+          p.exf[0] = (float)h->cfg.discount;
+          p.exf[1] = (float)(2.0 / (double)B);
+          cl.push_back(p);
+        }
+        TD3_RC(push_row_stage(h, P->tables, st, cl, kRowCriticLoss, Bp, "critic_loss"));
+      }
       std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0], true}, {&q2, Pq2, &P->Q[1], true}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true, kProCriticLoss,
-                            [&](GemmProb& p, int j) {
-                              const NetL& qt0 = q1;
-                              const NetL& qt1 = q2;
-                              const NetL& qj = j ? q2 : q1;
-                              p.ex[0] = P->TQ[0].H[2];
-                              p.ex[1] = P->TQ[1].H[2];
-                              p.ex[2] = P->Q[j].H[2];
-                              p.ex[3] = const_cast<float*>(Ptq1 + qt0.ln[2].offg);
-                              p.ex[4] = const_cast<float*>(Ptq2 + qt1.ln[2].offg);
-                              p.ex[5] = const_cast<float*>(Pq1 + qj.ln[2].offg);
-                              p.ex[6] = const_cast<float*>(Ptq1 + qt0.ln[2].offb);
-                              p.ex[7] = const_cast<float*>(Ptq2 + qt1.ln[2].offb);
-                              p.ex[8] = const_cast<float*>(Pq1 + qj.ln[2].offb);
-                              p.ex[9] = const_cast<float*>(Ptq1 + qt0.lin[3].offW);
-                              p.ex[10] = const_cast<float*>(Ptq2 + qt1.lin[3].offW);
-                              p.ex[11] = const_cast<float*>(Pq1 + qj.lin[3].offW);
-                              p.ex[12] = const_cast<float*>(Ptq1 + qt0.lin[3].offb);
-                              p.ex[13] = const_cast<float*>(Ptq2 + qt1.lin[3].offb);
-                              p.ex[14] = const_cast<float*>(Pq1 + qj.lin[3].offb);
-                              p.ex[15] = P->R;
-                              p.ex[16] = P->ND;
-                              p.ex[17] = P->Q[j].GZ[3];
-                              p.ex[18] = P->Q[j].GU[2];
-                              p.ex[19] = P->Q[j].U[2];
-                              p.ex[20] = P->Q[j].stats[2];
-                              p.ex[21] = P->Y;
-                              p.ex[22] = P->sqerr + (size_t)j * Bp;
-                              p.ex[23] = P->Q[j].Qv;
-                              p.exi[0] = qj.lin[2].N;
-                              p.exi[1] = qj.lin[2].Np;
-                              p.exi[2] = j;
-                              p.exf[0] = (float)h->cfg.discount;
-                              p.exf[1] = (float)(2.0 / (double)B);
-                            }));
+      TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true));
       TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0));
       if (!actor_phase) continue;
       // ---------------- delayed policy update (TD3_featured.py:156-171)
-      // Q1(s, pi(s)) forward, pi fused into layer 0
       std::vector<FwdItem> f3 = {{&q1, Pq1, &P->AQ, false, true}};
-      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0, kProPolicyHead,
-                            [&](GemmProb& p, int) {
-                              policy_head(p, Pa, P->A, P->X_S, 0);
-                              p.ex[7] = P->A.T;
-                              p.ex[8] = P->A.U[2];
-                              p.ex[9] = P->A.stats[2];
-                            }));
-      // -mean Q1 backward into Q1's layer 2, then dX through Q1 to its first layer
+      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0));
+      {
+        GemmProb p{};
+        p.norm = norm ? 1 : 0;
+        p.B = B;
+        p.ex[0] = P->AQ.H[2];
+        p.ex[1] = const_cast<float*>(Pq1 + q1.ln[2].offg);
+        p.ex[2] = const_cast<float*>(Pq1 + q1.ln[2].offb);
+        p.ex[3] = const_cast<float*>(Pq1 + q1.lin[3].offW);
+        p.ex[4] = const_cast<float*>(Pq1 + q1.lin[3].offb);
+        p.ex[5] = P->AQ.Qv;
+        p.Aout = P->AQ.GZ[2];
+        p.ldao = q1.lin[2].Np;
+        p.exi[0] = q1.lin[2].N;
+        p.exi[1] = q1.lin[2].Np;
+        p.exf[0] = (float)(-1.0) / (float)B;
+        std::vector<GemmProb> v = {p};
+        TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorLoss, Bp, "actor_loss"));
+      }
       std::vector<BwdItem> aqb = {{&q1, Pq1, &P->AQ, false}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false, kProActorLoss,
-                            [&](GemmProb& p, int) {
-                              p.ex[0] = P->AQ.H[2];
-                              p.ex[1] = const_cast<float*>(Pq1 + q1.ln[2].offg);
-                              p.ex[2] = const_cast<float*>(Pq1 + q1.ln[2].offb);
-                              p.ex[3] = const_cast<float*>(Pq1 + q1.lin[3].offW);
-                              p.ex[4] = const_cast<float*>(Pq1 + q1.lin[3].offb);
-                              p.ex[5] = P->AQ.Qv;
-                              p.exi[0] = q1.lin[2].N;
-                              p.exi[1] = q1.lin[2].Np;
-                              p.exf[0] = (float)(-1.0) / (float)B;
-                            }));
-      // dQ1/da -> actor head backward fused into the actor's layer-2 dX
+      TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false));
+      {
+        GemmProb p{};
+        p.norm = norm ? 1 : 0;
+        p.B = B;
+        p.ex[0] = P->AQ.GU[0];
+        p.ex[1] = P->AQ.H[0];
+        p.ex[2] = P->AQ.stats[0];
+        p.ex[3] = const_cast<float*>(Pq1 + q1.ln[0].offg);
+        p.ex[4] = const_cast<float*>(Pq1 + q1.lin[0].offW);
+        p.ex[5] = P->A.T;
+        p.ex[6] = const_cast<float*>(Pa + an.lin[3].offW);
+        p.ex[7] = P->A.H[2];
+        p.ex[8] = P->A.stats[2];
+        p.ex[9] = const_cast<float*>(Pa + an.ln[2].offg);
+        p.ex[10] = P->A.GZ[3];
+        p.ex[11] = P->A.GU[2];
+        p.Aout = P->A.GZ[2];
+        p.ldao = an.lin[2].Np;
+        p.exi[0] = q1.lin[0].N;
+        p.exi[1] = q1.lin[0].Np;
+        p.exi[2] = q1.lin[0].Kp;
+        p.exi[3] = sd;
+        p.exi[4] = ad;
+        p.exi[5] = an.lin[2].N;
+        p.exi[6] = an.lin[2].Np;
+        p.exi[7] = an.lin[3].Kp;
+        p.exf[0] = ma;
+        std::vector<GemmProb> v = {p};
+        TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorHeadBwd, Bp, "actor_head_bwd"));
+      }
       std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true, kProActorHeadBwd,
-                            [&](GemmProb& p, int) {
-                              p.ex[0] = P->AQ.GU[0];
-                              p.ex[1] = P->AQ.H[0];
-                              p.ex[2] = P->AQ.stats[0];
-                              p.ex[3] = const_cast<float*>(Pq1 + q1.ln[0].offg);
-                              p.ex[4] = const_cast<float*>(Pq1 + q1.lin[0].offW);
-                              p.ex[5] = P->A.T;
-                              p.ex[6] = const_cast<float*>(Pa + an.lin[3].offW);
-                              p.ex[7] = P->A.H[2];
-                              p.ex[8] = P->A.stats[2];
-                              p.ex[9] = const_cast<float*>(Pa + an.ln[2].offg);
-                              p.ex[10] = P->A.GZ[3];
-                              p.ex[11] = P->A.GU[2];
-                              p.exi[0] = q1.lin[0].N;
-                              p.exi[1] = q1.lin[0].Np;
-                              p.exi[2] = q1.lin[0].Kp;
-                              p.exi[3] = sd;
-                              p.exi[4] = ad;
-                              p.exi[5] = an.lin[2].N;
-                              p.exi[6] = an.lin[2].Np;
-                              p.exi[7] = an.lin[3].Kp;
-                              p.exf[0] = ma;
-                            }));
+      TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true));
       TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true));
     }
   }
