@@ -543,19 +543,30 @@ __device__ __forceinline__ void load_b(const GemmProb& P, float (&bv)[kMaxChunks
   }
 }
 
+// XCD-aware tile order (cdna_hip_programming.md §5.5 T1): the dispatcher deals blocks
+// round-robin over the 8 XCDs, so block b runs on XCD b % 8.  Consecutive tiles (which share
+// a weight column block: m is the fastest tile index) are given to blocks of one XCD, so a
+// weight tile is fetched over the fabric once per XCD and then hit in that XCD's L2.
+// `nb` is the real tile count; the grid is padded to a multiple of 8 (surplus blocks exit).
+__device__ __forceinline__ int xcd_tile(int nb) {
+  const int per = (nb + 7) >> 3;
+  return (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+}
+
 template <int MODE, int WN, int PRO>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict__ probs, int nprob,
-                                                      int Bp, Counters* bump, int bump_actor) {
+                                                      int Bp, Counters* bump, int bump_actor, int nb) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
   constexpr int WK = 4 / WN;
   constexpr bool kPrefetchB = true;
-  const int b = blockIdx.x;
-  if (bump && b == 0 && threadIdx.x == 0) {
+  const int b = xcd_tile(nb);
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     bump->total_it += 1;                       // TD3_featured.py:124
     bump->critic_step += 1;
     if (bump_actor) bump->actor_step += 1;
   }
+  if (b >= nb) return;
   int pi = 0;
   for (int i = 1; i < nprob; ++i)
     if (b >= probs[i].tile_begin) pi = i;
@@ -764,9 +775,10 @@ __device__ __forceinline__ void dw_load_chunk(const DwProb& P, int rc, int h, in
 // 4 waves, operands of the next row chunk in flight while the current one is multiplied).
 // Vector tiles: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU over 32 columns.
 // Both end in the fused optimizer update of the elements they own.
-__global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a) {
+__global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
   __shared__ float red[4 * 32 * 33];
-  const int b = blockIdx.x;
+  const int b = xcd_tile(nb);
+  if (b >= nb) return;
   int pi = 0;
   for (int i = 1; i < a.nprob; ++i)
     if (b >= a.probs[i].tile_begin) pi = i;
@@ -878,7 +890,9 @@ __global__ __launch_bounds__(256) void polyak_flat_kernel(float* T, const float*
 template <int MODE, int WN, int PRO>
 static void gl(const GemmProb* d, int nprob, int nblocks, int Bp, int lds, Counters* bump, int ba,
                hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(nblocks), dim3(256), lds, s, d, nprob, Bp, bump, ba);
+  const int padded = (nblocks + 7) & ~7;
+  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(256), lds, s, d, nprob, Bp, bump, ba,
+                     nblocks);
 }
 
 using GemmFn = void (*)(const GemmProb*, int, int, int, int, Counters*, int, hipStream_t);
@@ -955,7 +969,7 @@ int launch_lnbwd_rows(const LnBwdProb* d, int nprob, int Bp, int norm, hipStream
 
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s) {
   if (nblocks <= 0) return 0;
-  hipLaunchKernelGGL(dw_kernel, dim3(nblocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(dw_kernel, dim3((nblocks + 7) & ~7), dim3(256), 0, s, a, nblocks);
   TD3_HIP(hipGetLastError());
   return 0;
 }
