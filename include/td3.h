@@ -101,6 +101,7 @@ typedef struct td3_step_stats {
   float* q1;               /* nullable host [B] */
   float* q2;               /* nullable host [B] */
   int64_t* idx;            /* nullable host [B]: rows drawn */
+  float* noise;            /* nullable host [B][ad]: the N(0,1) draw of randn_like (:132) */
 } td3_step_stats;
 
 void td3_default_config(td3_config* cfg);

@@ -271,12 +271,15 @@ def featured_q(P, q, norm, s, a):
     return z, (lin, ln, cache)
 
 
-def featured_train_step(L: Learner, batch, noise, record=None):
+def featured_train_step(L: Learner, batch, noise, record=None, grad_hook=None):
     """One ``TD3_featured.TD3.train`` call (TD3_featured.py:123-171) on a gathered batch.
 
     ``batch`` = (state, action, next_state, reward, not_done) float32, ``noise`` =
-    the N(0,1) draw of ``torch.randn_like(action)`` (:132).
+    the N(0,1) draw of ``torch.randn_like(action)`` (:132).  ``grad_hook`` (data-parallel
+    restatement) maps each phase's gradient dict before its Adam step, e.g. an
+    all-reduce mean over ranks that each hold one shard of the global batch.
     """
+    hook = grad_hook if grad_hook is not None else (lambda g: g)
     rec = record if record is not None else {}
     s, a, s2, r, nd = batch
     B = s.shape[0]
@@ -300,7 +303,7 @@ def featured_train_step(L: Learner, batch, noise, record=None):
         g, _ = mlp_backward(lin, ln, cache, gq)
         grads.update(pack_mlp_grads(f"{q}.", g, L.norm))
     rec["critic_grads"] = grads
-    L.adam_critic(grads)                                                       # :151-153
+    L.adam_critic(hook(grads))                                                 # :151-153
     if L.total_it % L.policy_freq == 0:                                        # :156
         pi, (alin, aln, acache, t) = featured_actor(L.actor, L.norm, L.max_action, s)
         aq1, (qlin, qln, qcache) = featured_q(L.critic, "q1", L.norm, s, pi)   # :159
@@ -312,7 +315,7 @@ def featured_train_step(L: Learner, batch, noise, record=None):
         ag, _ = mlp_backward(alin, aln, acache, gz.astype(f32))
         agrads = pack_mlp_grads("", ag, L.norm)
         rec["actor_grads"] = agrads
-        L.adam_actor(agrads)                                                   # :162-164
+        L.adam_actor(hook(agrads))                                             # :162-164
         L.polyak()                                                             # :167-171
     return rec
 

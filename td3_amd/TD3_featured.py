@@ -307,8 +307,10 @@ class TD3(TD3_base):
             q1 = np.empty(B, np.float32)
             q2 = np.empty(B, np.float32)
             idx = np.empty(B, np.int64)
-            keep = [y, q1, q2, idx]
+            drawn = np.empty((B, self.action_dim), np.float32)
+            keep = [y, q1, q2, idx, drawn]
             st.y, st.q1, st.q2, st.idx = (y.ctypes.data, q1.ctypes.data, q2.ctypes.data, idx.ctypes.data)
+            st.noise = drawn.ctypes.data
         nz = None
         if noise is not None:
             nz = np.ascontiguousarray(np.asarray(noise, dtype=np.float32).reshape(B, self.action_dim))
@@ -334,7 +336,7 @@ class TD3(TD3_base):
         if st is None:
             return None
         out = {"critic_loss": st.critic_loss, "actor_step": bool(st.actor_step),
-               "y": keep[0], "q1": keep[1], "q2": keep[2], "idx": keep[3]}
+               "y": keep[0], "q1": keep[1], "q2": keep[2], "idx": keep[3], "noise": keep[4]}
         if st.actor_step:
             out["actor_loss"] = st.actor_loss
         return out

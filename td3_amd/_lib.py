@@ -33,7 +33,8 @@ class td3_config(C.Structure):
 
 class td3_step_stats(C.Structure):
     _fields_ = [("critic_loss", C.c_double), ("actor_loss", C.c_double), ("actor_step", C.c_int),
-                ("y", C.c_void_p), ("q1", C.c_void_p), ("q2", C.c_void_p), ("idx", C.c_void_p)]
+                ("y", C.c_void_p), ("q1", C.c_void_p), ("q2", C.c_void_p), ("idx", C.c_void_p),
+                ("noise", C.c_void_p)]
 
 
 _P = C.c_void_p
@@ -110,6 +111,7 @@ def load(path: str = LIB_PATH):
     # libhsa-runtime64.so.1 / librccl.so.1 resolve to those already-loaded copies, so the
     # process has ONE HIP runtime and torch streams / pointers are valid in our calls.
     import torch  # noqa: F401
+    path = os.environ.get("TD3_LIB", path)       # kernel-variant experiments (tools/)
     if not os.path.exists(path):
         raise ImportError(
             f"libtd3hip.so not found at {path}: build it with `python -m td3_amd.build` "

@@ -1,6 +1,6 @@
-// Problem descriptors of the TD3 step kernels (device-memory tables, read with
-// scalar loads by every workgroup; pointers are fixed for the handle's life so
-// the launches can be captured once into a hipGraph and replayed).
+// Problem descriptors of the TD3 step kernels (kernel-argument tables, read with scalar
+// loads by every workgroup; pointers are fixed for the handle's life so the launches can
+// be captured once into a hipGraph and replayed).
 #pragma once
 #include "common.h"
 
@@ -51,6 +51,14 @@ struct GemmProb {
   float exf[4];
   uint64_t seed;
   const Counters* ctr;
+};
+
+// Problems of one GEMM / row launch, passed BY VALUE in the kernel arguments (one scalar
+// load level fewer than a device table at the head of every workgroup's dependency chain).
+constexpr int kMaxProbs = 4;
+struct GemmTable {
+  GemmProb p[kMaxProbs];
+  int nprob;
 };
 
 // ------------------------------------------------------------------ row-wise heads (act / eval_q)
@@ -106,16 +114,17 @@ struct AdamArgs {
   float grad_scale;                                   // 1/world for the all-reduced path
 };
 
+constexpr int kMaxDwProbs = 8;     // 4 layers x 2 networks (twin critic)
 struct DwArgs {
-  const DwProb* probs; int nprob; int Bp;
+  DwProb probs[kMaxDwProbs]; int nprob; int Bp;
   AdamArgs adam;
   int mode;
 };
 
 // ------------------------------------------------------------------ launchers (kernels.hip)
-int launch_gemm(int mode, int wn, int pro, const GemmProb* d_probs, int nprob, int nblocks, int Bp,
-                int lds_bytes, Counters* bump, int bump_actor, hipStream_t s);
-int launch_rows(int kind, const GemmProb* d_probs, int nprob, int Bp, hipStream_t s);
+int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds_bytes,
+                Counters* bump, int bump_actor, hipStream_t s);
+int launch_rows(int kind, const GemmTable& t, int Bp, hipStream_t s);
 int launch_heads(const HeadArgs& a, int nprob, hipStream_t s);
 int launch_lnbwd_rows(const LnBwdProb* d_probs, int nprob, int Bp, int norm, hipStream_t s);
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s);

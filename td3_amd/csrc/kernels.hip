@@ -26,6 +26,10 @@
 
 #include "kernels.h"
 
+#ifndef TD3_EXP
+#define TD3_EXP 0   // timing experiments only (tools/): 1 no LN math, 2 no MFMA, 3 no weight loads
+#endif
+
 namespace td3 {
 
 // ================================================================== helpers
@@ -217,7 +221,11 @@ __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx
     rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * 8 + r) * P.lda, P.Kp, c.lane);
   rv_load(g, P.lng, P.Kp, c.lane);
   rv_load(bb, P.lnb, P.Kp, c.lane);
+#if TD3_EXP == 1
+  for (int r = 0; r < RB; ++r) { mean[r] = g[0]; rstd[r] = bb[0]; }
+#else
   ln_fwd_rows<RB>(x, g, bb, P.Kreal, c.lane, mean, rstd);
+#endif
   const bool t0 = c.nt == 0;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
@@ -500,8 +508,8 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
 }
 
 template <int KIND>
-__global__ __launch_bounds__(256) void row_kernel(const GemmProb* __restrict__ probs, int Bp) {
-  const GemmProb P = probs[blockIdx.y];
+__global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
+  const GemmProb& P = tab.p[blockIdx.y];
   const RowCtx c{(int)(blockIdx.x * 4 + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
   if (c.row >= Bp) return;
   if constexpr (KIND == kRowPolicyHead) row_policy_head(P, c);
@@ -554,8 +562,8 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 }
 
 template <int MODE, int WN, int PRO>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict__ probs, int nprob,
-                                                      int Bp, Counters* bump, int bump_actor, int nb) {
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmTable tab, int Bp, Counters* bump, int bump_actor,
+                                                      int nb) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
   constexpr int WK = 4 / WN;
@@ -568,9 +576,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict
   }
   if (b >= nb) return;
   int pi = 0;
-  for (int i = 1; i < nprob; ++i)
-    if (b >= probs[i].tile_begin) pi = i;
-  const GemmProb P = probs[pi];   // fields to registers before any store
+#pragma unroll
+  for (int i = 1; i < kMaxProbs; ++i)
+    if (i < tab.nprob && b >= tab.p[i].tile_begin) pi = i;
+  const GemmProb& P = tab.p[pi];
   const int mtiles = Bp >> 5;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
@@ -588,8 +597,15 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict
   const int ncol = (active ? ncol0 : 0) + i;
 
   float bv[kMaxChunks][16];
+  // bias of the epilogue's column, requested with the weights (off the tail of the chain)
+  const int bcol = (WK == 1) ? ncol : n0 + (threadIdx.x & 31);
+  const float bias = (MODE == 0 && P.bias && (WK > 1 || active)) ? gld(P.bias + bcol) : 0.f;
   if constexpr (kPrefetchB) {
+#if TD3_EXP == 3
+    for (int cc = 0; cc < kMaxChunks; ++cc) for (int q = 0; q < 16; ++q) bv[cc][q] = (float)(q + cc);
+#else
     load_b<MODE>(P, bv, cb, nch, ncol, h);
+#endif
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
   }
 
@@ -614,8 +630,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict
           const float4 v = *reinterpret_cast<const float4*>(arow + kb + 4 * q);
           av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
         }
+#if TD3_EXP == 2
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc[s] += av[s] * bv[cc][s];
+#else
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[cc][s], acc);
+#endif
       }
     }
   }
@@ -623,7 +644,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict
   if constexpr (WK == 1) {
     if (active) {
       const int col = ncol0 + i;
-      const float bias = (MODE == 0 && P.bias) ? gld(P.bias + (col)) : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = mfma_row(r, lane);
@@ -646,7 +666,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmProb* __restrict
       float v = red[row * 33 + col];
 #pragma unroll
       for (int w = 1; w < 4; ++w) v = v + red[(w * 32 + row) * 33 + col];
-      if (MODE == 0 && P.bias) v = v + gld(P.bias + (n0 + col));
+      if (MODE == 0 && P.bias) v = v + bias;
       if (P.relu) v = fmaxf(v, 0.f);
       gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + col), v);
     }
@@ -780,9 +800,10 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
   const int b = xcd_tile(nb);
   if (b >= nb) return;
   int pi = 0;
-  for (int i = 1; i < a.nprob; ++i)
-    if (b >= a.probs[i].tile_begin) pi = i;
-  const DwProb P = a.probs[pi];
+#pragma unroll
+  for (int i = 1; i < kMaxDwProbs; ++i)
+    if (i < a.nprob && b >= a.probs[i].tile_begin) pi = i;
+  const DwProb& P = a.probs[pi];
   const int t = b - P.tile_begin;
   const int nmat = (P.Np >> 5) * P.ntk;
   const AdamK k = make_adam(a.adam);
@@ -888,14 +909,12 @@ __global__ __launch_bounds__(256) void polyak_flat_kernel(float* T, const float*
 
 // ================================================================== launchers
 template <int MODE, int WN, int PRO>
-static void gl(const GemmProb* d, int nprob, int nblocks, int Bp, int lds, Counters* bump, int ba,
-               hipStream_t s) {
+static void gl(const GemmTable& t, int nblocks, int Bp, int lds, Counters* bump, int ba, hipStream_t s) {
   const int padded = (nblocks + 7) & ~7;
-  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(256), lds, s, d, nprob, Bp, bump, ba,
-                     nblocks);
+  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(256), lds, s, t, Bp, bump, ba, nblocks);
 }
 
-using GemmFn = void (*)(const GemmProb*, int, int, int, int, Counters*, int, hipStream_t);
+using GemmFn = void (*)(const GemmTable&, int, int, int, Counters*, int, hipStream_t);
 
 // Forward stages use Copy / LN / the two policy heads; input-grad stages use LN-bwd and the
 // three loss heads.  Only those combinations are instantiated.
@@ -925,7 +944,7 @@ static GemmFn pick_gemm(int mode, int wn, int pro) {
   return nullptr;
 }
 
-int launch_gemm(int mode, int wn, int pro, const GemmProb* d, int nprob, int nblocks, int Bp, int lds,
+int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds,
                 Counters* bump, int bump_actor, hipStream_t s) {
   if (nblocks <= 0) return 0;
   GemmFn f = pick_gemm(mode, wn, pro);
@@ -933,13 +952,13 @@ int launch_gemm(int mode, int wn, int pro, const GemmProb* d, int nprob, int nbl
     set_error("launch_gemm: unsupported mode %d wn %d pro %d", mode, wn, pro);
     return -1;
   }
-  f(d, nprob, nblocks, Bp, lds, bump, bump_actor, s);
+  f(t, nblocks, Bp, lds, bump, bump_actor, s);
   TD3_HIP(hipGetLastError());
   return 0;
 }
 
-int launch_rows(int kind, const GemmProb* d, int nprob, int Bp, hipStream_t s) {
-  const dim3 grid(Bp / 4, nprob);
+int launch_rows(int kind, const GemmTable& d, int Bp, hipStream_t s) {
+  const dim3 grid(Bp / 4, d.nprob);
   switch (kind) {
     case kRowPolicyHead: hipLaunchKernelGGL(row_kernel<kRowPolicyHead>, grid, dim3(256), 0, s, d, Bp); break;
     case kRowCriticLoss: hipLaunchKernelGGL(row_kernel<kRowCriticLoss>, grid, dim3(256), 0, s, d, Bp); break;

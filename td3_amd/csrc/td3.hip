@@ -142,6 +142,9 @@ struct Plan {
   // stage lists (excluding the input stage): [actor_phase][inject_noise]
   std::vector<Stage> body[2][2];
   hipGraphExec_t graph[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  // the same bodies with the replay-ring gather captured in front (Philox draw path)
+  hipGraphExec_t graph_g[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  const void* graph_ring = nullptr;
 };
 
 struct ActPlan {       // select_action / eval_q at small batch
@@ -221,29 +224,31 @@ static int push_gemm_stage(td3_handle* h, std::vector<void*>& owned, std::vector
                            std::vector<GemmProb>& probs, int mode, int wn, int pro, int Bp, int lds,
                            int blocks, double flops, const std::string& name, Counters* bump,
                            int bump_actor) {
-  void* d = nullptr;
-  TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
-  const int np = (int)probs.size();
-  const GemmProb* dp = (const GemmProb*)d;
+  (void)h;
+  (void)owned;
+  TD3_ARG(!probs.empty() && probs.size() <= (size_t)kMaxProbs, "too many problems in one gemm stage");
+  GemmTable t{};
+  for (size_t i = 0; i < probs.size(); ++i) t.p[i] = probs[i];
+  t.nprob = (int)probs.size();
   char kname[64];
   snprintf(kname, sizeof(kname), "td3::gemm_kernel<%d, %d, %d>", mode, wn, pro);
   st.push_back({name,
-                [=](hipStream_t s) {
-                  return launch_gemm(mode, wn, pro, dp, np, blocks, Bp, lds, bump, bump_actor, s);
-                },
+                [=](hipStream_t s) { return launch_gemm(mode, wn, pro, t, blocks, Bp, lds, bump, bump_actor, s); },
                 flops, kname});
   return 0;
 }
 
 static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           std::vector<GemmProb>& probs, int kind, int Bp, const std::string& name) {
-  void* d = nullptr;
-  TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(GemmProb), &d));
-  const int np = (int)probs.size();
-  const GemmProb* dp = (const GemmProb*)d;
+  (void)h;
+  (void)owned;
+  TD3_ARG(!probs.empty() && probs.size() <= (size_t)kMaxProbs, "too many problems in one row stage");
+  GemmTable t{};
+  for (size_t i = 0; i < probs.size(); ++i) t.p[i] = probs[i];
+  t.nprob = (int)probs.size();
   char kname[64];
   snprintf(kname, sizeof(kname), "td3::row_kernel<%d>", kind);
-  st.push_back({name, [=](hipStream_t s) { return launch_rows(kind, dp, np, Bp, s); }, 0, kname});
+  st.push_back({name, [=](hipStream_t s) { return launch_rows(kind, t, Bp, s); }, 0, kname});
   return 0;
 }
 
@@ -424,10 +429,9 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       probs.push_back(p);
     }
   }
-  void* d = nullptr;
-  TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(DwProb), &d));
+  TD3_ARG(probs.size() <= (size_t)kMaxDwProbs, "too many problems in one dw stage");
   DwArgs a{};
-  a.probs = (const DwProb*)d;
+  for (size_t i = 0; i < probs.size(); ++i) a.probs[i] = probs[i];
   a.nprob = (int)probs.size();
   a.Bp = Bp;
   a.adam.P = g.P;
@@ -478,9 +482,12 @@ static void free_plan_tables(std::vector<void*>& t) {
 
 static void destroy_plan(Plan* p) {
   if (!p) return;
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b)
+  for (int a = 0; a < 2; ++a) {
+    for (int b = 0; b < 2; ++b) {
       if (p->graph[a][b]) hipGraphExecDestroy(p->graph[a][b]);
+      if (p->graph_g[a][b]) hipGraphExecDestroy(p->graph_g[a][b]);
+    }
+  }
   free_plan_tables(p->tables);
   if (p->scratch) hipFree(p->scratch);
 }
@@ -771,17 +778,32 @@ static int input_from_batch(td3_handle* h, Plan* P, const float* s, const float*
   return 0;
 }
 
-static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s) {
+// One step body on stream s.  With `ring` set, the replay-ring gather (Philox draw) is
+// launched first and, in graph mode, captured into the same hipGraph (one replay per step).
+static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring* ring) {
   Plan* P = h->plan.get();
   std::vector<Stage>& st = P->body[actor_phase][inj];
   h->last_body = &st;
-  if (!h->cfg.use_graph) return run_stages(st, s);
-  hipGraphExec_t& ge = P->graph[actor_phase][inj];
+  if (!h->cfg.use_graph) {
+    if (ring) TD3_RC(input_from_ring(h, ring, P, false, s));
+    return run_stages(st, s);
+  }
+  if (ring && P->graph_ring != ring) {          // graphs bake the ring's pointers in
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b)
+        if (P->graph_g[a][b]) {
+          TD3_HIP(hipGraphExecDestroy(P->graph_g[a][b]));
+          P->graph_g[a][b] = nullptr;
+        }
+    P->graph_ring = ring;
+  }
+  hipGraphExec_t& ge = ring ? P->graph_g[actor_phase][inj] : P->graph[actor_phase][inj];
   if (!ge) {
     hipStream_t cs;
     TD3_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     TD3_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    int rc = run_stages(st, cs);
+    int rc = ring ? input_from_ring(h, ring, P, false, cs) : 0;
+    if (!rc) rc = run_stages(st, cs);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(cs, &g);
     if (rc) {
@@ -833,6 +855,7 @@ static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_s
   if (stats->q1) TD3_HIP(hipMemcpy(stats->q1, P->Q[0].Qv, B * 4, hipMemcpyDeviceToHost));
   if (stats->q2) TD3_HIP(hipMemcpy(stats->q2, P->Q[1].Qv, B * 4, hipMemcpyDeviceToHost));
   if (stats->idx) TD3_HIP(hipMemcpy(stats->idx, P->d_idx, B * 8, hipMemcpyDeviceToHost));
+  if (stats->noise) TD3_HIP(hipMemcpy(stats->noise, P->noise, (size_t)B * h->ad * 4, hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -1145,8 +1168,12 @@ int td3_train_step(td3_handle* h, rb_handle* rbh, int batch, void* stream, const
   if (inject_noise)
     TD3_HIP(hipMemcpyAsync(P->noise, inject_noise, (size_t)batch * h->ad * 4, hipMemcpyHostToDevice, s));
   const int actor_phase = ((h->total_it + 1) % h->cfg.policy_freq) == 0;
-  TD3_RC(input_from_ring(h, r, P, inject_idx != nullptr, s));
-  TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s));
+  if (inject_idx) {
+    TD3_RC(input_from_ring(h, r, P, true, s));
+    TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s, nullptr));
+  } else {
+    TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s, r));
+  }
   if (inject_idx || inject_noise) TD3_HIP(hipStreamSynchronize(s));   // host sources are pageable
   return finish_step(h, actor_phase, s, stats);
 }
@@ -1165,7 +1192,7 @@ int td3_train_step_batch(td3_handle* h, const float* state, const float* action,
     TD3_HIP(hipMemcpyAsync(P->noise, inject_noise, (size_t)batch * h->ad * 4, hipMemcpyHostToDevice, s));
   const int actor_phase = ((h->total_it + 1) % h->cfg.policy_freq) == 0;
   TD3_RC(input_from_batch(h, P, state, action, next_state, reward, not_done, s));
-  TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s));
+  TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s, nullptr));
   if (inject_noise) TD3_HIP(hipStreamSynchronize(s));
   return finish_step(h, actor_phase, s, stats);
 }

@@ -202,3 +202,51 @@ def test_foreign_buffer_path():
     out = pol.train_step(Foreign(), S["B"], noise=noise, stats=True)
     assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5
     _params_close(pol.critic.numpy_dict(), L.critic, 1e-4, "critic")
+
+
+def test_philox_graph_path_teacher_forced():
+    """The production path (Philox draws, gather captured in the step graph): the rows and
+    noise it drew are read back, the oracle replays the same step, and the results agree."""
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    seen = set()
+    for step in range(1, 5):
+        _load_oracle_state(pol, L)
+        out = pol.train_step(rb, S["B"], stats=True)
+        idx, noise = out["idx"], out["noise"]
+        assert idx.min() >= 0 and idx.max() < gen.BUFFER_ROWS
+        assert np.isfinite(noise).all() and 0.5 < noise.std() < 1.5
+        seen.add(idx.tobytes())
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5, step
+        assert _rel_to_max(out["q1"], rec["q1"][:, 0]) <= 1e-5, step
+        np.testing.assert_allclose(out["critic_loss"], rec["critic_loss"], rtol=1e-5)
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (step, "critic"))
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (step, "critic_target"))
+    assert len(seen) == 4                                   # a fresh draw every step
+
+
+def test_allreduce_path_single_rank():
+    """The data-parallel kernels (grad-only dW, RCCL all-reduce, flat Adam + Polyak) at
+    nranks = 1 against the oracle, teacher-forced like the fused path."""
+    import ctypes as C
+    from td3_amd import _lib
+    G = load_golden("featured", "hc_layer")
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    uid = (C.c_ubyte * 128)()
+    _lib.check(pol._lib.td3_comm_unique_id(uid), "td3_comm_unique_id")
+    _lib.check(pol._lib.td3_comm_init(pol._h, uid, 1, 0), "td3_comm_init")
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    for step in range(1, 5):
+        p = f"step{step}"
+        _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(G[f"{p}/idx"]), G[f"{p}/noise"])
+        out = pol.train_step(rb, S["B"], indices=G[f"{p}/idx"], noise=G[f"{p}/noise"], stats=True)
+        assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5, p
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (p, "critic"))
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (p, "actor"))
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"))
+        _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"))
