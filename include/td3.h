@@ -12,12 +12,14 @@
  *   rb_add               ReplayBuffer_featured.add        my_replay_buffer.py:109-117
  *   rb_sample            ReplayBuffer_featured.sample     my_replay_buffer.py:119-128
  *   rb_read/write_records ReplayBuffer_featured.save/load my_replay_buffer.py:91-107
+ *   rb_*_particles       ReplayBuffer_particles          my_replay_buffer.py:6-69
  *   td3_create           TD3.__init__ + TD3_base.__init__ TD3_featured.py:100-110, TD3_base.py:7-24
  *   td3_get/set_params   state_dict()/load_state_dict()   TD3_base.py:26-50 (save/load)
  *   td3_train_step       TD3.train(replay_buffer, B)      TD3_featured.py:123-171
  *   td3_train_step_batch TD3.train on a foreign buffer's sample() tensors
  *   td3_select_action    TD3.select_action                TD3_featured.py:113-115
  *   td3_eval_q           TD3.eval_q                       TD3_featured.py:117-121
+ *   td3_*_particles      TD3_particles.TD3 (set encoder)  TD3_particles.py:136-224
  *
  * Ownership: handles own all device memory.  Host pointers are owned by the caller
  * and only read/written during the call.  Device pointers passed in (rb_sample
@@ -49,6 +51,7 @@ typedef struct rb_info_t {
   int64_t max_size, ptr, size;
   void* data;              /* device pointer of the ring [max_size][record_floats] */
   int device;
+  int n_particles, particle_dim;   /* particle rings (state_dim = feature dim); 0 otherwise */
 } rb_info_t;
 
 int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint64_t seed,
@@ -73,6 +76,19 @@ int rb_write_records(rb_handle* h, int64_t start, int64_t n, const float* in, in
                      int64_t size);
 int rb_sync(rb_handle* h);
 
+/* TD3_particles ring (ReplayBuffer_particles, my_replay_buffer.py:6-69).  Record:
+ * [feat(F) | particles(N*D) | action(A) | next_feat(F) | next_particles(N*D) | r | not_done | pad]. */
+int rb_create_particles(int feat_dim, int n_particles, int particle_dim, int action_dim, int64_t max_size,
+                        int device, uint64_t seed, rb_handle** out);
+/* float64 host rows: feat [n][F], part [n][N][D], action [n][A], ... (my_replay_buffer.py:46-56) */
+int rb_add_particles(rb_handle* h, const double* feat, const double* part, const double* action,
+                     const double* next_feat, const double* next_part, const double* reward,
+                     const double* done, int64_t n, void* stream);
+/* The 7 tensors of ReplayBuffer_particles.sample (:58-69) into device outputs. */
+int rb_sample_particles(rb_handle* h, int batch, float* feat, float* part, float* action, float* next_feat,
+                        float* next_part, float* reward, float* not_done, const int64_t* inject_idx,
+                        int64_t* idx_out, void* stream);
+
 /* ------------------------------------------------------------------ learner */
 typedef struct td3_config {
   int state_dim, action_dim;
@@ -86,6 +102,11 @@ typedef struct td3_config {
   uint64_t seed;           /* Philox key for index draws and target-policy noise */
   int device;
   int use_graph;           /* capture each step variant into a hipGraph (default 1) */
+  /* TD3_particles (TD3_particles.py): state = (features [F], particles [N][D]); the Q head has
+   * action_dim outputs; state_dim = F, hidden widths (500, 400, 300) for actor and critic. */
+  int particles;           /* 0: TD3_featured, 1: TD3_particles */
+  int n_particles, particle_dim;
+  int cdq;                 /* clipped double-Q (CDQ flag, TD3_particles.py:126-133); featured: twin always */
 } td3_config;
 
 enum td3_which {
@@ -93,7 +114,7 @@ enum td3_which {
   TD3_ACTOR_ADAM_M = 4, TD3_ACTOR_ADAM_V = 5, TD3_CRITIC_ADAM_M = 6, TD3_CRITIC_ADAM_V = 7
 };
 
-typedef struct td3_step_stats {
+typedef struct td3_step_stats {   /* particles: y / q1 / q2 are [B][action_dim] */
   double critic_loss;      /* mse(Q1,y) + mse(Q2,y)  (TD3_featured.py:148) */
   double actor_loss;       /* -mean Q1(s, pi(s)) on actor steps, else NaN (:159) */
   int actor_step;          /* 1 when the delayed policy update ran (:156) */
@@ -134,6 +155,17 @@ int td3_train_step_batch(td3_handle* h, const float* state, const float* action,
 int td3_select_action(td3_handle* h, const float* state, float* action_out, int n);
 /* (state, action) (host) -> q_out[2*n] = Q1, Q2; synchronous. */
 int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_out, int n);
+
+/* TD3_particles (TD3_particles.py:153-164, 167-224). */
+int td3_train_step_batch_particles(td3_handle* h, const float* feat, const float* part, const float* action,
+                                   const float* next_feat, const float* next_part, const float* reward,
+                                   const float* not_done, int batch, void* stream, const float* inject_noise,
+                                   td3_step_stats* stats);
+/* host feat [n][F], part [n][N][D] -> action_out [n][A] (tanh policy) */
+int td3_select_action_particles(td3_handle* h, const float* feat, const float* part, float* action_out, int n);
+/* -> q_out [2][n][A] (Q1, then Q2; Q2 = Q1 when CDQ is off) */
+int td3_eval_q_particles(td3_handle* h, const float* feat, const float* part, const float* action, float* q_out,
+                         int n);
 
 /* ------------------------------------------------------------------ multi-GPU (RCCL) */
 int td3_comm_unique_id(unsigned char out[128]);

@@ -17,7 +17,8 @@ LIB_PATH = os.path.join(_HERE, "libtd3hip.so")
 class rb_info_t(C.Structure):
     _fields_ = [("state_dim", C.c_int), ("action_dim", C.c_int), ("record_floats", C.c_int),
                 ("max_size", C.c_int64), ("ptr", C.c_int64), ("size", C.c_int64),
-                ("data", C.c_void_p), ("device", C.c_int)]
+                ("data", C.c_void_p), ("device", C.c_int),
+                ("n_particles", C.c_int), ("particle_dim", C.c_int)]
 
 
 class td3_config(C.Structure):
@@ -28,7 +29,8 @@ class td3_config(C.Structure):
                 ("noise_clip", C.c_double), ("policy_freq", C.c_int),
                 ("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double),
                 ("eps", C.c_double), ("seed", C.c_uint64), ("device", C.c_int),
-                ("use_graph", C.c_int)]
+                ("use_graph", C.c_int), ("particles", C.c_int), ("n_particles", C.c_int),
+                ("particle_dim", C.c_int), ("cdq", C.c_int)]
 
 
 class td3_step_stats(C.Structure):
@@ -54,6 +56,10 @@ SIGNATURES = {
     "rb_read_records": (C.c_int, [_P, C.c_int64, C.c_int64, _F]),
     "rb_write_records": (C.c_int, [_P, C.c_int64, C.c_int64, _F, C.c_int64, C.c_int64]),
     "rb_sync": (C.c_int, [_P]),
+    "rb_create_particles": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_uint64,
+                                      C.POINTER(_P)]),
+    "rb_add_particles": (C.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, C.c_int64, _P]),
+    "rb_sample_particles": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "td3_default_config": (None, [C.POINTER(td3_config)]),
     "td3_create": (C.c_int, [C.POINTER(td3_config), C.POINTER(_P)]),
     "td3_destroy": (C.c_int, [_P]),
@@ -69,6 +75,10 @@ SIGNATURES = {
                                        C.POINTER(td3_step_stats)]),
     "td3_select_action": (C.c_int, [_P, _F, _F, C.c_int]),
     "td3_eval_q": (C.c_int, [_P, _F, _F, _F, C.c_int]),
+    "td3_train_step_batch_particles": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_int, _P, _F,
+                                                 C.POINTER(td3_step_stats)]),
+    "td3_select_action_particles": (C.c_int, [_P, _F, _F, _F, C.c_int]),
+    "td3_eval_q_particles": (C.c_int, [_P, _F, _F, _F, _F, C.c_int]),
     "td3_comm_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
     "td3_comm_init": (C.c_int, [_P, C.POINTER(C.c_ubyte), C.c_int, C.c_int]),
     "td3_sync": (C.c_int, [_P]),

@@ -15,7 +15,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 OUT = os.path.join(HERE, "libtd3hip.so")
-SOURCES = ["csrc/replay.hip", "csrc/kernels.hip", "csrc/td3.hip"]
+SOURCES = ["csrc/replay.hip", "csrc/kernels.hip", "csrc/encoder.hip", "csrc/td3.hip"]
 ARCH = os.environ.get("TD3_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
          "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value"]

@@ -1,0 +1,209 @@
+// Device helpers shared by the TD3 step kernels (kernels.hip) and the particle encoder
+// (encoder.hip): DPP wave sums, global-address-space accessors, lane-sliced row vectors
+// and the LayerNorm row forward / backward.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+namespace td3 {
+
+// ================================================================== helpers
+// Wave64 sum, result uniform: DPP within each 16-lane row, then the four rows via readlane.
+__device__ __forceinline__ float wsum(float v) {
+  int x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false)); // row_half_mirror
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false)); // row_mirror
+  x = __float_as_int(v);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(x, 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(x, 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(x, 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(x, 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
+// Global-address-space accessors: pointers read from problem tables are generic to the
+// compiler, which would otherwise emit flat_* loads (counted on vmcnt AND lgkmcnt, so
+// every s_load wait also drains them).  These force global_load / global_store.
+#define GAS __attribute__((address_space(1)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 gld4(const float* p) {
+  const f32x4 v = *(const GAS f32x4*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float gld(const float* p) { return *(const GAS float*)p; }
+__device__ __forceinline__ void gst4(float* p, float4 v) {
+  f32x4 w;
+  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+  *(GAS f32x4*)p = w;
+}
+__device__ __forceinline__ void gst(float* p, float v) { *(GAS float*)p = v; }
+
+// A lane's slice of a row of width <= 512: v[4q+e] = row[lane*4 + 256q + e].
+__device__ __forceinline__ int rcol(int lane, int j) { return lane * 4 + ((j >> 2) << 8) + (j & 3); }
+
+__device__ __forceinline__ void rv_load(float (&v)[8], const float* __restrict__ row, int n, int lane) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  const float4 a = gld4(row + (c0 < n ? c0 : 0));
+  const float4 b = gld4(row + (c1 < n ? c1 : 0));
+  const bool va = c0 < n, vb = c1 < n;
+  v[0] = va ? a.x : 0.f; v[1] = va ? a.y : 0.f; v[2] = va ? a.z : 0.f; v[3] = va ? a.w : 0.f;
+  v[4] = vb ? b.x : 0.f; v[5] = vb ? b.y : 0.f; v[6] = vb ? b.z : 0.f; v[7] = vb ? b.w : 0.f;
+}
+
+__device__ __forceinline__ void rv_store(float* __restrict__ row, int n, int lane, const float (&v)[8]) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  if (c0 < n) gst4(row + c0, make_float4(v[0], v[1], v[2], v[3]));
+  if (c1 < n) gst4(row + c1, make_float4(v[4], v[5], v[6], v[7]));
+}
+
+__device__ __forceinline__ void rv_load_lds(float (&v)[8], const float* row, int n, int lane) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  const float4 a = *reinterpret_cast<const float4*>(row + (c0 < n ? c0 : 0));
+  const float4 b = *reinterpret_cast<const float4*>(row + (c1 < n ? c1 : 0));
+  const bool va = c0 < n, vb = c1 < n;
+  v[0] = va ? a.x : 0.f; v[1] = va ? a.y : 0.f; v[2] = va ? a.z : 0.f; v[3] = va ? a.w : 0.f;
+  v[4] = vb ? b.x : 0.f; v[5] = vb ? b.y : 0.f; v[6] = vb ? b.z : 0.f; v[7] = vb ? b.w : 0.f;
+}
+
+// LDS row store (generic float4 store into shared memory).
+__device__ __forceinline__ void lds_store8(float* row, int n, int lane, const float (&v)[8]) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  if (c0 < n) *reinterpret_cast<float4*>(row + c0) = make_float4(v[0], v[1], v[2], v[3]);
+  if (c1 < n) *reinterpret_cast<float4*>(row + c1) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+__device__ __forceinline__ float rv_psum(const float (&v)[8], int K, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (rcol(lane, j) < K) s += v[j];
+  return s;
+}
+
+__device__ __forceinline__ float rv_pdot(const float (&a)[8], const float (&b)[8], int K, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (rcol(lane, j) < K) s += a[j] * b[j];
+  return s;
+}
+
+// LayerNorm (torch CPU formula: y = (x*rstd + (-mean*rstd))*gamma + beta), RB rows at once.
+template <int RB>
+__device__ __forceinline__ void ln_fwd_rows(float (&x)[RB][8], const float (&g)[8], const float (&bb)[8],
+                                            int K, int lane, float (&mean)[RB], float (&rstd)[RB]) {
+  float s[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) s[r] = rv_psum(x[r], K, lane);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) mean[r] = wsum(s[r]) / (float)K;
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (rcol(lane, j) < K) {
+        const float d = x[r][j] - mean[r];
+        v += d * d;
+      }
+    s[r] = v;
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rstd[r] = 1.0f / sqrtf(wsum(s[r]) / (float)K + 1e-5f);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const float nb = -mean[r] * rstd[r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      x[r][j] = rcol(lane, j) < K ? (x[r][j] * rstd[r] + nb) * g[j] + bb[j] : 0.f;
+  }
+}
+
+// dZ = relu'(h) * LN_bwd(dU): gx = gu*gamma; dh = rstd*((gx - mean(gx)) - xhat*mean(gx*xhat)).
+// RELU = false: the LayerNorm input is not a ReLU output (TD3_particles lnorm1 on the
+// concatenated [pooled | features | action] row), so no relu' mask is applied.
+template <int RB, bool RELU = true>
+__device__ __forceinline__ void ln_bwd_rows(float (&gu)[RB][8], const float (&h)[RB][8], const float (&g)[8],
+                                            const float (&mean)[RB], const float (&rstd)[RB], int K,
+                                            int lane, int norm) {
+  if (!norm) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gu[r][j] = (!RELU || h[r][j] > 0.f) ? gu[r][j] : 0.f;
+    return;
+  }
+  float xh[RB][8], s1[RB], s2[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    s1[r] = 0.f;
+    s2[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xh[r][j] = (h[r][j] - mean[r]) * rstd[r];
+      gu[r][j] = gu[r][j] * g[j];
+      if (rcol(lane, j) < K) {
+        s1[r] += gu[r][j];
+        s2[r] += gu[r][j] * xh[r][j];
+      }
+    }
+  }
+  float m1[RB], m2[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    m1[r] = wsum(s1[r]) / (float)K;
+    m2[r] = wsum(s2[r]) / (float)K;
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      gu[r][j] = ((!RELU || h[r][j] > 0.f) && rcol(lane, j) < K)
+                     ? rstd[r] * ((gu[r][j] - m1[r]) - xh[r][j] * m2[r])
+                                                      : 0.f;
+}
+
+// ================================================================== Adam
+struct AdamK {
+  float w1, b2, c2, bc2s, negss, eps, tau, omt, gscale;
+};
+
+__device__ __forceinline__ AdamK make_adam(const AdamArgs& a) {
+  AdamK k;
+  const int64_t step = a.which ? a.ctr->actor_step : a.ctr->critic_step;
+  const double bc1 = 1.0 - pow(a.beta1, (double)step);
+  const double bc2 = 1.0 - pow(a.beta2, (double)step);
+  k.negss = (float)(-(a.lr / bc1));
+  k.bc2s = (float)sqrt(bc2);
+  k.w1 = (float)(1.0 - a.beta1);
+  k.b2 = (float)a.beta2;
+  k.c2 = (float)(1.0 - a.beta2);
+  k.eps = (float)a.eps;
+  k.tau = a.tau;
+  k.omt = (float)(1.0 - (double)a.tau);
+  k.gscale = a.grad_scale;
+  return k;
+}
+
+// torch _single_tensor_adam (adam.py:520-547): lerp, mul/addcmul, sqrt/div/add, addcdiv.
+__device__ __forceinline__ void adam_elem(float* __restrict__ p, float* __restrict__ m,
+                                          float* __restrict__ v, float g, const AdamK& k,
+                                          float* __restrict__ t) {
+  float mm = gld(m), vv = gld(v), pp = gld(p);
+  mm = __fmaf_rn(k.w1, g - mm, mm);
+  vv = vv * k.b2;
+  vv = vv + (k.c2 * g) * g;
+  const float denom = sqrtf(vv) / k.bc2s + k.eps;
+  pp = pp + (k.negss * mm) / denom;
+  gst(m, mm);
+  gst(v, vv);
+  gst(p, pp);
+  if (t) gst(t, k.tau * pp + k.omt * gld(t));     // TD3_featured.py:167-171
+}
+
+}  // namespace td3

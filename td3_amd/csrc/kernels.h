@@ -24,7 +24,10 @@ enum RowKind : int {
   kRowPolicyHead = 0,    // a' = clamp(ma*tanh(head(LN3(H3))) + clip(eps)) or pi = ma*tanh(...)
   kRowCriticLoss = 1,    // min(Q1',Q2') target, mse grad, Q head and LN3 backward of Q_j
   kRowActorLoss = 2,     // -mean Q1(s, pi(s)): head and LN3 backward of Q1
-  kRowActorHeadBwd = 3   // dQ1/da (Q1 LN1 bwd, W1 action cols), tanh bwd, actor head + LN3 bwd
+  kRowActorHeadBwd = 3,  // dQ1/da (Q1 LN1 bwd, W1 action cols), tanh bwd, actor head + LN3 bwd
+  kRowCriticLossP = 4,   // TD3_particles: the same over A Q outputs, optional CDQ
+  kRowActorLossP = 5,    // TD3_particles: -mean over B*A
+  kRowActorHeadBwdP = 6  // TD3_particles: dQ1/da through lnorm1, tanh bwd, actor head + LN3 bwd
 };
 
 constexpr int kMaxEx = 24;
@@ -71,7 +74,7 @@ struct HeadProb {
   float* stats;                              // nullable: store LN3 (mean, rstd) [2][Bp]
   const float* W4; int ldw; const float* b4; int nout;
   int mode;
-  float* out; int ldo; int out_col;
+  float* out; int ldo; int out_col;   // policy: out[row*ldo + out_col + o]; Q: out[row*ldo + o]
   float* tanh_out;
   float* noise; int ldn;
 };
@@ -114,7 +117,7 @@ struct AdamArgs {
   float grad_scale;                                   // 1/world for the all-reduced path
 };
 
-constexpr int kMaxDwProbs = 8;     // 4 layers x 2 networks (twin critic)
+constexpr int kMaxDwProbs = 10;    // (4 layers + input LayerNorm) x 2 networks (twin critic)
 struct DwArgs {
   DwProb probs[kMaxDwProbs]; int nprob; int Bp;
   AdamArgs adam;

@@ -24,6 +24,7 @@
 // (exact fp32 FMA chain, MI355X_MICROARCH.md § Matrix cores).
 #include <math.h>
 
+#include "dev.h"
 #include "kernels.h"
 
 #ifndef TD3_EXP
@@ -31,164 +32,6 @@
 #endif
 
 namespace td3 {
-
-// ================================================================== helpers
-// Wave64 sum, result uniform: DPP within each 16-lane row, then the four rows via readlane.
-__device__ __forceinline__ float wsum(float v) {
-  int x = __float_as_int(v);
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-  x = __float_as_int(v);
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
-  x = __float_as_int(v);
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false)); // row_half_mirror
-  x = __float_as_int(v);
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false)); // row_mirror
-  x = __float_as_int(v);
-  const float r0 = __int_as_float(__builtin_amdgcn_readlane(x, 0));
-  const float r1 = __int_as_float(__builtin_amdgcn_readlane(x, 16));
-  const float r2 = __int_as_float(__builtin_amdgcn_readlane(x, 32));
-  const float r3 = __int_as_float(__builtin_amdgcn_readlane(x, 48));
-  return (r0 + r1) + (r2 + r3);
-}
-
-// Global-address-space accessors: pointers read from problem tables are generic to the
-// compiler, which would otherwise emit flat_* loads (counted on vmcnt AND lgkmcnt, so
-// every s_load wait also drains them).  These force global_load / global_store.
-#define GAS __attribute__((address_space(1)))
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 gld4(const float* p) {
-  const f32x4 v = *(const GAS f32x4*)p;
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float gld(const float* p) { return *(const GAS float*)p; }
-__device__ __forceinline__ void gst4(float* p, float4 v) {
-  f32x4 w;
-  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
-  *(GAS f32x4*)p = w;
-}
-__device__ __forceinline__ void gst(float* p, float v) { *(GAS float*)p = v; }
-
-// A lane's slice of a row of width <= 512: v[4q+e] = row[lane*4 + 256q + e].
-__device__ __forceinline__ int rcol(int lane, int j) { return lane * 4 + ((j >> 2) << 8) + (j & 3); }
-
-__device__ __forceinline__ void rv_load(float (&v)[8], const float* __restrict__ row, int n, int lane) {
-  const int c0 = lane * 4, c1 = c0 + 256;
-  const float4 a = gld4(row + (c0 < n ? c0 : 0));
-  const float4 b = gld4(row + (c1 < n ? c1 : 0));
-  const bool va = c0 < n, vb = c1 < n;
-  v[0] = va ? a.x : 0.f; v[1] = va ? a.y : 0.f; v[2] = va ? a.z : 0.f; v[3] = va ? a.w : 0.f;
-  v[4] = vb ? b.x : 0.f; v[5] = vb ? b.y : 0.f; v[6] = vb ? b.z : 0.f; v[7] = vb ? b.w : 0.f;
-}
-
-__device__ __forceinline__ void rv_store(float* __restrict__ row, int n, int lane, const float (&v)[8]) {
-  const int c0 = lane * 4, c1 = c0 + 256;
-  if (c0 < n) gst4(row + c0, make_float4(v[0], v[1], v[2], v[3]));
-  if (c1 < n) gst4(row + c1, make_float4(v[4], v[5], v[6], v[7]));
-}
-
-__device__ __forceinline__ void rv_load_lds(float (&v)[8], const float* row, int n, int lane) {
-  const int c0 = lane * 4, c1 = c0 + 256;
-  const float4 a = *reinterpret_cast<const float4*>(row + (c0 < n ? c0 : 0));
-  const float4 b = *reinterpret_cast<const float4*>(row + (c1 < n ? c1 : 0));
-  const bool va = c0 < n, vb = c1 < n;
-  v[0] = va ? a.x : 0.f; v[1] = va ? a.y : 0.f; v[2] = va ? a.z : 0.f; v[3] = va ? a.w : 0.f;
-  v[4] = vb ? b.x : 0.f; v[5] = vb ? b.y : 0.f; v[6] = vb ? b.z : 0.f; v[7] = vb ? b.w : 0.f;
-}
-
-// LDS row store (generic float4 store into shared memory).
-__device__ __forceinline__ void lds_store8(float* row, int n, int lane, const float (&v)[8]) {
-  const int c0 = lane * 4, c1 = c0 + 256;
-  if (c0 < n) *reinterpret_cast<float4*>(row + c0) = make_float4(v[0], v[1], v[2], v[3]);
-  if (c1 < n) *reinterpret_cast<float4*>(row + c1) = make_float4(v[4], v[5], v[6], v[7]);
-}
-
-__device__ __forceinline__ float rv_psum(const float (&v)[8], int K, int lane) {
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    if (rcol(lane, j) < K) s += v[j];
-  return s;
-}
-
-__device__ __forceinline__ float rv_pdot(const float (&a)[8], const float (&b)[8], int K, int lane) {
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    if (rcol(lane, j) < K) s += a[j] * b[j];
-  return s;
-}
-
-// LayerNorm (torch CPU formula: y = (x*rstd + (-mean*rstd))*gamma + beta), RB rows at once.
-template <int RB>
-__device__ __forceinline__ void ln_fwd_rows(float (&x)[RB][8], const float (&g)[8], const float (&bb)[8],
-                                            int K, int lane, float (&mean)[RB], float (&rstd)[RB]) {
-  float s[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) s[r] = rv_psum(x[r], K, lane);
-#pragma unroll
-  for (int r = 0; r < RB; ++r) mean[r] = wsum(s[r]) / (float)K;
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    float v = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (rcol(lane, j) < K) {
-        const float d = x[r][j] - mean[r];
-        v += d * d;
-      }
-    s[r] = v;
-  }
-#pragma unroll
-  for (int r = 0; r < RB; ++r) rstd[r] = 1.0f / sqrtf(wsum(s[r]) / (float)K + 1e-5f);
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    const float nb = -mean[r] * rstd[r];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      x[r][j] = rcol(lane, j) < K ? (x[r][j] * rstd[r] + nb) * g[j] + bb[j] : 0.f;
-  }
-}
-
-// dZ = relu'(h) * LN_bwd(dU): gx = gu*gamma; dh = rstd*((gx - mean(gx)) - xhat*mean(gx*xhat)).
-template <int RB>
-__device__ __forceinline__ void ln_bwd_rows(float (&gu)[RB][8], const float (&h)[RB][8], const float (&g)[8],
-                                            const float (&mean)[RB], const float (&rstd)[RB], int K,
-                                            int lane, int norm) {
-  if (!norm) {
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) gu[r][j] = h[r][j] > 0.f ? gu[r][j] : 0.f;
-    return;
-  }
-  float xh[RB][8], s1[RB], s2[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    s1[r] = 0.f;
-    s2[r] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      xh[r][j] = (h[r][j] - mean[r]) * rstd[r];
-      gu[r][j] = gu[r][j] * g[j];
-      if (rcol(lane, j) < K) {
-        s1[r] += gu[r][j];
-        s2[r] += gu[r][j] * xh[r][j];
-      }
-    }
-  }
-  float m1[RB], m2[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    m1[r] = wsum(s1[r]) / (float)K;
-    m2[r] = wsum(s2[r]) / (float)K;
-  }
-#pragma unroll
-  for (int r = 0; r < RB; ++r)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      gu[r][j] = (h[r][j] > 0.f && rcol(lane, j) < K) ? rstd[r] * ((gu[r][j] - m1[r]) - xh[r][j] * m2[r])
-                                                      : 0.f;
-}
 
 __device__ __forceinline__ void lds_put_row(float* smem, int S, int row, int Kp, int lane, const float (&v)[8]) {
   lds_store8(smem + row * S, Kp, lane, v);
@@ -277,8 +120,9 @@ struct RowCtx {
 // ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=W4 ex[4]=b4 ex[5]=noise
 // out: ex[6]=critic input rows (action columns at sd..) ex[7]=T ex[8]=U3 ex[9]=stats3
 // exi[0]=K3 exi[1]=ld3 exi[2]=ldw4 exi[3]=ld_out exi[4]=gen_noise exi[5]=ad exi[6]=sd exi[7]=ldn
-// exi[8]=target (1: smoothing + clamp; 0: policy)
-// exf[0]=max_action exf[1]=policy_noise exf[2]=noise_clip
+// exi[8]=target (1: smoothing; 0: policy) exi[9]=clamp a' to +-max_action (TD3_featured :135-137;
+// TD3_particles :179-181 has no clamp)   ex[10]=second critic-input buffer for a' (nullable)
+// exf[0]=max_action (1 for TD3_particles: tanh output, :68) exf[1]=policy_noise exf[2]=noise_clip
 constexpr int kHeadRegs = 8;   // head outputs kept in registers (wider heads loop)
 
 __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx& c) {
@@ -341,12 +185,13 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
     float n = z * P.exf[1];
     n = fminf(fmaxf(n, -P.exf[2]), P.exf[2]);
     const float v = ma * th + n;
-    a = fminf(fmaxf(v, -ma), ma);
+    a = P.exi[9] ? fminf(fmaxf(v, -ma), ma) : v;
   } else {
     a = ma * th;
     gst(P.ex[7] + ((size_t)c.row * 32 + o), th);
   }
   gst(P.ex[6] + ((size_t)c.row * P.exi[3] + sd + o), live ? a : 0.f);
+  if (P.ex[10]) gst(P.ex[10] + ((size_t)c.row * P.exi[3] + sd + o), live ? a : 0.f);
 }
 
 // ---- clipped double-Q target + critic mse backward into LN3 of Q_j -----------------------
@@ -507,6 +352,162 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
 }
 
+// ================================================================== TD3_particles heads
+// The Q networks of TD3_particles output one value per action dimension (Q head [A, 300],
+// TD3_particles.py:91); y = r + not_done*discount*min(Q1', Q2') broadcasts over them (:183-189)
+// and F.mse_loss averages over B*A.  Values / targets are kept as [Bp][32] rows.
+
+// ex[0..2]=H3 of (target q1, target q2 (= target q1 when CDQ is off), online q_j)
+// ex[3..5]=gamma3 ex[6..8]=beta3 ex[9..11]=W4 [nq][ldw4] ex[12..14]=b4 ex[15]=reward ex[16]=not_done
+// out: ex[17]=dZ4_j (ld 32) ex[18]=dU3_j ex[19]=U3_j ex[20]=stats3_j ex[21]=y [Bp][32]
+//      ex[22]=sqerr_j (sum over outputs) ex[23]=Q_j [Bp][32]   Aout=dZ3_j
+// exi[0]=K3 exi[1]=ld3 exi[2]=j exi[3]=nq exi[4]=ldw4 exi[5]=cdq   exf[0]=discount exf[1]=2/(B*nq)
+__device__ __forceinline__ void row_critic_loss_p(const GemmProb& P, const RowCtx& c) {
+  const int K3 = P.exi[0], ld3 = P.exi[1], j = P.exi[2], nq = P.exi[3], ldw4 = P.exi[4];
+  const bool cdq = P.exi[5] != 0;
+  float x0[1][8], x1[1][8], xq[1][8], h[1][8], g[3][8], bb[3][8];
+  rv_load(x0[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
+  rv_load(x1[0], P.ex[1] + (size_t)c.row * ld3, ld3, c.lane);
+  rv_load(xq[0], P.ex[2] + (size_t)c.row * ld3, ld3, c.lane);
+  if (P.norm) {
+#pragma unroll
+    for (int n = 0; n < 3; ++n) {
+      rv_load(g[n], P.ex[3 + n], ld3, c.lane);
+      rv_load(bb[n], P.ex[6 + n], ld3, c.lane);
+    }
+  }
+  const float rw = gld(P.ex[15] + c.row), nd = gld(P.ex[16] + c.row);
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) h[0][jj] = xq[0][jj];
+  float m0[1], s0[1], m1[1], s1[1], mq[1], sq[1];
+  if (P.norm) {
+    ln_fwd_rows<1>(x0, g[0], bb[0], K3, c.lane, m0, s0);
+    ln_fwd_rows<1>(x1, g[1], bb[1], K3, c.lane, m1, s1);
+    ln_fwd_rows<1>(xq, g[2], bb[2], K3, c.lane, mq, sq);
+  } else {
+    mq[0] = 0.f;
+    sq[0] = 1.f;
+  }
+  const bool live = c.row < P.B;
+  float gu[1][8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) gu[0][jj] = 0.f;
+  float se = 0.f;
+  for (int o = 0; o < nq; ++o) {
+    float w0[8], w1[8], wq[8];
+    rv_load(w0, P.ex[9] + (size_t)o * ldw4, ld3, c.lane);
+    rv_load(w1, P.ex[10] + (size_t)o * ldw4, ld3, c.lane);
+    rv_load(wq, P.ex[11] + (size_t)o * ldw4, ld3, c.lane);
+    const float tq0 = wsum(rv_pdot(x0[0], w0, K3, c.lane)) + gld(P.ex[12] + o);
+    const float tq1 = cdq ? wsum(rv_pdot(x1[0], w1, K3, c.lane)) + gld(P.ex[13] + o) : tq0;
+    const float q = wsum(rv_pdot(xq[0], wq, K3, c.lane)) + gld(P.ex[14] + o);
+    const float y = rw + (nd * P.exf[0]) * fminf(tq0, tq1);          // TD3_particles.py:183-189
+    const float d = q - y;
+    const float gq = live ? P.exf[1] * d : 0.f;                       // mse over B*A
+    se += live ? d * d : 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) gu[0][jj] += gq * wq[jj];
+    if (c.lane == 0) {
+      gst(P.ex[17] + ((size_t)c.row * 32 + o), gq);
+      gst(P.ex[23] + ((size_t)c.row * 32 + o), q);
+      if (j == 0) gst(P.ex[21] + ((size_t)c.row * 32 + o), y);
+    }
+  }
+  if (c.lane == 0) {
+    gst(P.ex[22] + c.row, se);
+    if (P.norm) {
+      gst(P.ex[20] + c.row, mq[0]);
+      gst(P.ex[20] + (c.Bp + c.row), sq[0]);
+    }
+  }
+  rv_store(P.ex[18] + (size_t)c.row * ld3, ld3, c.lane, gu[0]);
+  if (P.norm) rv_store(P.ex[19] + (size_t)c.row * ld3, ld3, c.lane, xq[0]);
+  ln_bwd_rows<1>(gu, h, g[2], mq, sq, K3, c.lane, P.norm);
+  rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
+}
+
+// -mean over B*nq of Q1(s, pi(s)) (TD3_particles.py:211-212), head + LN3 backward of Q1.
+// ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=W4 ex[4]=b4  out ex[5]=Q [Bp][32], Aout=dZ3
+// exi[0]=K3 exi[1]=ld3 exi[2]=nq exi[3]=ldw4   exf[0]=-1/(B*nq)
+__device__ __forceinline__ void row_actor_loss_p(const GemmProb& P, const RowCtx& c) {
+  const int K3 = P.exi[0], ld3 = P.exi[1], nq = P.exi[2], ldw4 = P.exi[3];
+  float x[1][8], h[1][8], g[8], bb[8], mean[1], rstd[1];
+  rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
+  if (P.norm) {
+    rv_load(g, P.ex[1], ld3, c.lane);
+    rv_load(bb, P.ex[2], ld3, c.lane);
+  }
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) h[0][jj] = x[0][jj];
+  if (P.norm) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+  const float gq = c.row < P.B ? P.exf[0] : 0.f;
+  float gu[1][8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) gu[0][jj] = 0.f;
+  for (int o = 0; o < nq; ++o) {
+    float w[8];
+    rv_load(w, P.ex[3] + (size_t)o * ldw4, ld3, c.lane);
+    const float q = wsum(rv_pdot(x[0], w, K3, c.lane)) + gld(P.ex[4] + o);
+    if (c.lane == 0) gst(P.ex[5] + ((size_t)c.row * 32 + o), q);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) gu[0][jj] += gq * w[jj];
+  }
+  ln_bwd_rows<1>(gu, h, g, mean, rstd, K3, c.lane, P.norm);
+  rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
+}
+
+// dQ1/da through lnorm1 (the Q input LayerNorm, no ReLU before it), tanh backward (no
+// max_action, TD3_particles.py:68), then the actor head and LN3 backward.
+// ex[0]=dU_in of Q1(s,pi) (grad of the lnorm1 output) ex[1]=X of Q1(s,pi) ex[2]=lnorm1 stats
+// ex[3]=lnorm1 gamma (q1) ex[5]=T (tanh out, [Bp][32]) ex[6]=W4 (actor) ex[7]=H3 (actor)
+// ex[8]=stats3 (actor) ex[9]=gamma3 (actor)   out: ex[10]=dZ4 actor (ld 32) ex[11]=dU3 actor, Aout=dZ3
+// exi[0]=Kin exi[1]=ld_in exi[3]=first action column exi[4]=ad exi[5]=K3 exi[6]=ld3 exi[7]=ldw4
+// exf[0]=max_action scale of the policy output
+__device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const RowCtx& c) {
+  const int Kin = P.exi[0], ldin = P.exi[1], acol = P.exi[3], ad = P.exi[4];
+  const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
+  const float ma = P.exf[0];
+  float gu[1][8], xr[1][8], gi[8], h3[1][8], g3[8], mi[1], ri[1], mn3[1], rs3[1];
+  rv_load(gu[0], P.ex[0] + (size_t)c.row * ldin, ldin, c.lane);
+  rv_load(xr[0], P.ex[1] + (size_t)c.row * ldin, ldin, c.lane);
+  rv_load(h3[0], P.ex[7] + (size_t)c.row * ld3, ld3, c.lane);
+  if (P.norm) {
+    rv_load(gi, P.ex[3], ldin, c.lane);
+    rv_load(g3, P.ex[9], ld3, c.lane);
+    mi[0] = gld(P.ex[2] + c.row);
+    ri[0] = gld(P.ex[2] + (c.Bp + c.row));
+    mn3[0] = gld(P.ex[8] + c.row);
+    rs3[0] = gld(P.ex[8] + (c.Bp + c.row));
+  } else {
+    mi[0] = mn3[0] = 0.f;
+    ri[0] = rs3[0] = 1.f;
+  }
+  const float tl = c.lane < ad ? gld(P.ex[5] + ((size_t)c.row * 32 + c.lane)) : 0.f;
+  ln_bwd_rows<1, false>(gu, xr, gi, mi, ri, Kin, c.lane, P.norm);     // grad of the Q input row
+  const bool live = c.row < P.B;
+  float gu3[1][8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) gu3[0][jj] = 0.f;
+  for (int o = 0; o < ad; ++o) {
+    const int col = acol + o;                                         // rcol^-1: lane, register
+    const int jsel = ((col >> 8) << 2) + (col & 3);
+    float v = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) v = jj == jsel ? gu[0][jj] : v;
+    const float ga = __shfl(v, (col & 255) >> 2, 64);
+    const float t = __shfl(tl, o, 64);
+    const float gz4 = live ? (ga * ma) * (1.f - t * t) : 0.f;
+    if (c.lane == 0) gst(P.ex[10] + ((size_t)c.row * 32 + o), gz4);
+    float w4[8];
+    rv_load(w4, P.ex[6] + (size_t)o * ldw4, ld3, c.lane);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4[jj];
+  }
+  rv_store(P.ex[11] + (size_t)c.row * ld3, ld3, c.lane, gu3[0]);
+  ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, P.norm);
+  rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
+}
+
 template <int KIND>
 __global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
   const GemmProb& P = tab.p[blockIdx.y];
@@ -516,6 +517,9 @@ __global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
   else if constexpr (KIND == kRowCriticLoss) row_critic_loss(P, c);
   else if constexpr (KIND == kRowActorLoss) row_actor_loss(P, c);
   else if constexpr (KIND == kRowActorHeadBwd) row_actor_head_bwd(P, c);
+  else if constexpr (KIND == kRowCriticLossP) row_critic_loss_p(P, c);
+  else if constexpr (KIND == kRowActorLossP) row_actor_loss_p(P, c);
+  else if constexpr (KIND == kRowActorHeadBwdP) row_actor_head_bwd_p(P, c);
 }
 
 // ================================================================== batch-row GEMM stage
@@ -707,7 +711,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     gst(P.out + ((size_t)row * P.ldo + P.out_col + o), live ? a.max_action * th : 0.f);
     if (P.tanh_out) gst(P.tanh_out + ((size_t)row * 32 + o), th);
   } else {
-    if (o == 0) gst(P.out + (row), zl);
+    gst(P.out + ((size_t)row * P.ldo + o), zl);          // Q values [row][nout]
   }
 }
 
@@ -732,44 +736,7 @@ __global__ __launch_bounds__(256) void lnbwd_rows_kernel(const LnBwdProb* __rest
   for (int r = 0; r < RB; ++r) rv_store(P.GZ + (size_t)(row0 + r) * P.ld, P.ld, lane, gu[r]);
 }
 
-// ================================================================== Adam / Polyak
-struct AdamK {
-  float w1, b2, c2, bc2s, negss, eps, tau, omt, gscale;
-};
-
-__device__ __forceinline__ AdamK make_adam(const AdamArgs& a) {
-  AdamK k;
-  const int64_t step = a.which ? a.ctr->actor_step : a.ctr->critic_step;
-  const double bc1 = 1.0 - pow(a.beta1, (double)step);
-  const double bc2 = 1.0 - pow(a.beta2, (double)step);
-  k.negss = (float)(-(a.lr / bc1));
-  k.bc2s = (float)sqrt(bc2);
-  k.w1 = (float)(1.0 - a.beta1);
-  k.b2 = (float)a.beta2;
-  k.c2 = (float)(1.0 - a.beta2);
-  k.eps = (float)a.eps;
-  k.tau = a.tau;
-  k.omt = (float)(1.0 - (double)a.tau);
-  k.gscale = a.grad_scale;
-  return k;
-}
-
-// torch _single_tensor_adam (adam.py:520-547): lerp, mul/addcmul, sqrt/div/add, addcdiv.
-__device__ __forceinline__ void adam_elem(float* __restrict__ p, float* __restrict__ m,
-                                          float* __restrict__ v, float g, const AdamK& k,
-                                          float* __restrict__ t) {
-  float mm = gld(m), vv = gld(v), pp = gld(p);
-  mm = __fmaf_rn(k.w1, g - mm, mm);
-  vv = vv * k.b2;
-  vv = vv + (k.c2 * g) * g;
-  const float denom = sqrtf(vv) / k.bc2s + k.eps;
-  pp = pp + (k.negss * mm) / denom;
-  gst(m, mm);
-  gst(v, vv);
-  gst(p, pp);
-  if (t) gst(t, k.tau * pp + k.omt * gld(t));     // TD3_featured.py:167-171
-}
-
+// ================================================================== Adam / Polyak (AdamK, adam_elem: dev.h)
 __device__ __forceinline__ void apply_grad(const DwArgs& a, const AdamK& k, int64_t idx, float g) {
   if (a.mode == kDwGrad) {
     gst(a.adam.G + (idx), g);
@@ -846,13 +813,14 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
   const int n0 = (t - nmat) * 32;
   const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const bool ln = P.offg >= 0;
+  const bool hasb = P.offb >= 0;                    // false: a LayerNorm-only problem (lnorm1)
   float sb = 0.f, sg = 0.f, sbeta = 0.f;
   for (int r0 = rg; r0 < a.Bp; r0 += 64) {
     float gz[8], gu[8], hh[8], mu[8], rs[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int r = min(r0 + 8 * u, a.Bp - 1);      // clamped: loads stay unconditional
-      gz[u] = gld(P.G + ((size_t)r * P.ldg + n0 + c));
+      gz[u] = hasb ? gld(P.G + ((size_t)r * P.ldg + n0 + c)) : 0.f;
       if (ln) {
         gu[u] = gld(P.GU + ((size_t)r * P.ldgu + n0 + c));
         hh[u] = gld(P.H + ((size_t)r * P.ldh + n0 + c));
@@ -885,7 +853,7 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
       s1 += red[(1 * 8 + g) * 32 + c];
       s2 += red[(2 * 8 + g) * 32 + c];
     }
-    apply_grad(a, k, P.offb + n0 + c, s0);
+    if (hasb) apply_grad(a, k, P.offb + n0 + c, s0);
     if (ln) {
       apply_grad(a, k, P.offg + n0 + c, s1);
       apply_grad(a, k, P.offbeta + n0 + c, s2);
@@ -965,6 +933,11 @@ int launch_rows(int kind, const GemmTable& d, int Bp, hipStream_t s) {
     case kRowActorLoss: hipLaunchKernelGGL(row_kernel<kRowActorLoss>, grid, dim3(256), 0, s, d, Bp); break;
     case kRowActorHeadBwd:
       hipLaunchKernelGGL(row_kernel<kRowActorHeadBwd>, grid, dim3(256), 0, s, d, Bp);
+      break;
+    case kRowCriticLossP: hipLaunchKernelGGL(row_kernel<kRowCriticLossP>, grid, dim3(256), 0, s, d, Bp); break;
+    case kRowActorLossP: hipLaunchKernelGGL(row_kernel<kRowActorLossP>, grid, dim3(256), 0, s, d, Bp); break;
+    case kRowActorHeadBwdP:
+      hipLaunchKernelGGL(row_kernel<kRowActorHeadBwdP>, grid, dim3(256), 0, s, d, Bp);
       break;
     default:
       set_error("launch_rows: unknown kind %d", kind);

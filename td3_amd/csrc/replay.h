@@ -8,10 +8,16 @@ namespace td3 {
 //   [ state(sd) | action(ad) | next_state(sd) | reward | not_done | pad to 16 B ]
 // (the reference keeps 5 float64 SoA arrays, my_replay_buffer.py:81-85; one
 // record per row makes the sample gather one contiguous read per index).
+// TD3_particles rings (ReplayBuffer_particles, my_replay_buffer.py:6-69) use the record
+//   [ features(F) | particles(N*D) | action(A) | next_features(F) | next_particles(N*D) |
+//     reward | not_done | pad ]
+// with sd = F, ad = A; the learner's encoder reads the particle blocks in place (no gather).
 struct Ring {
   int sd = 0, ad = 0;
   int rec = 0;
   int o_s = 0, o_a = 0, o_s2 = 0, o_r = 0, o_nd = 0;
+  int particles = 0, N = 0, D = 0;  // particle rings only
+  int o_p = 0, o_p2 = 0;
   int64_t cap = 0;
   int64_t ptr = 0, size = 0;       // host mirror of my_replay_buffer.py:76-77
   float* data = nullptr;           // [cap][rec]
@@ -33,8 +39,9 @@ struct GatherSeg {
   int ld, col, src, len;
 };
 
-constexpr int kMaxSegs = 10;
-constexpr int kMaxRecord = 2048;   // floats per record the gather stages in LDS (2*sd+ad+2 <= 2048)
+constexpr int kMaxSegs = 12;
+constexpr int kMaxRecord = 2048;   // records up to this width are staged whole in LDS; wider
+                                   // records (particle rings) are gathered segment by segment
 struct GatherArgs {
   GatherSeg seg[kMaxSegs];
   int nseg;

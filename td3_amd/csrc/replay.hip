@@ -5,6 +5,8 @@
 //   ReplayBuffer_featured.add       :109-117 -> rb_add (batched, pinned staging, async H2D)
 //   ReplayBuffer_featured.sample    :119-128 -> rb_sample / gather_kernel (Philox + HBM gather)
 //   ReplayBuffer_featured.save/load :91-107  -> rb_read_records / rb_write_records
+//   ReplayBuffer_particles          :6-69    -> rb_create_particles / rb_add_particles /
+//                                               rb_sample_particles (same ring, wider record)
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
@@ -19,40 +21,56 @@ namespace td3 {
 // (rec floats, 16-B aligned) is read as float4 and scattered into every
 // destination segment.  Rows B..Bp-1 are zero-filled so padded batch rows stay
 // finite and contribute nothing downstream.
+__device__ __forceinline__ int64_t gather_row_index(const GatherArgs& a, int row) {
+  if (a.inject_idx) return a.inject_idx[row];
+  const uint64_t step = a.ctr ? (uint64_t)(a.ctr->total_it + 1) : a.step;
+  return (int64_t)philox_index(a.seed, step, (uint32_t)row, (uint64_t)*a.d_size);
+}
+
+template <bool STAGED>
 __global__ __launch_bounds__(256) void gather_kernel(GatherArgs a) {
-  __shared__ float rec_lds[4][kMaxRecord];
+  __shared__ float rec_lds[STAGED ? 4 : 1][STAGED ? kMaxRecord : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + wave;
   if (row >= a.Bp) return;
-  float* lr = rec_lds[wave];
-  if (row < a.B) {
-    int64_t idx;
-    if (a.inject_idx) {
-      idx = a.inject_idx[row];
+  if constexpr (STAGED) {
+    float* lr = rec_lds[wave];
+    if (row < a.B) {
+      const int64_t idx = gather_row_index(a, row);
+      if (a.idx_out && lane == 0) a.idx_out[row] = idx;
+      // the whole record first (every load in flight), then the scatter into the segments
+      const float4* src = reinterpret_cast<const float4*>(a.data + (size_t)idx * a.rec);
+      for (int c = lane; c < (a.rec >> 2); c += 64) reinterpret_cast<float4*>(lr)[c] = src[c];
     } else {
-      const uint64_t step = a.ctr ? (uint64_t)(a.ctr->total_it + 1) : a.step;
-      idx = (int64_t)philox_index(a.seed, step, (uint32_t)row, (uint64_t)*a.d_size);
+      for (int c = lane; c < a.rec; c += 64) lr[c] = 0.f;          // padded rows stay zero
     }
-    if (a.idx_out && lane == 0) a.idx_out[row] = idx;
-    // the whole record first (every load in flight), then the scatter into the segments
-    const float4* src = reinterpret_cast<const float4*>(a.data + (size_t)idx * a.rec);
-    for (int c = lane; c < (a.rec >> 2); c += 64) reinterpret_cast<float4*>(lr)[c] = src[c];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    for (int s = 0; s < a.nseg; ++s) {
+      const GatherSeg g = a.seg[s];
+      float* d = g.dst + (size_t)row * g.ld + g.col;
+      for (int c = lane; c < g.len; c += 64) d[c] = row < a.B ? lr[g.src + c] : 0.f;
+    }
   } else {
-    for (int c = lane; c < a.rec; c += 64) lr[c] = 0.f;          // padded rows stay zero
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  for (int s = 0; s < a.nseg; ++s) {
-    const GatherSeg g = a.seg[s];
-    float* d = g.dst + (size_t)row * g.ld + g.col;
-    for (int c = lane; c < g.len; c += 64) d[c] = row < a.B ? lr[g.src + c] : 0.f;
+    const float* src = nullptr;
+    if (row < a.B) {
+      const int64_t idx = gather_row_index(a, row);
+      if (a.idx_out && lane == 0) a.idx_out[row] = idx;
+      src = a.data + (size_t)idx * a.rec;
+    }
+    for (int s = 0; s < a.nseg; ++s) {
+      const GatherSeg g = a.seg[s];
+      float* d = g.dst + (size_t)row * g.ld + g.col;
+      for (int c = lane; c < g.len; c += 64) d[c] = src ? src[g.src + c] : 0.f;
+    }
   }
 }
 
 int launch_gather(const GatherArgs& a, hipStream_t s) {
   if (a.Bp <= 0) return 0;
   dim3 grid((a.Bp + 3) / 4);
-  hipLaunchKernelGGL(gather_kernel, grid, dim3(256), 0, s, a);
+  if (a.rec <= kMaxRecord) hipLaunchKernelGGL(gather_kernel<true>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(gather_kernel<false>, grid, dim3(256), 0, s, a);
   TD3_HIP(hipGetLastError());
   return 0;
 }
@@ -60,15 +78,14 @@ int launch_gather(const GatherArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------ synthetic fill
 // state, next_state ~ N(0,1); action ~ U(-max_action, max_action);
 // reward ~ N(0,1); not_done = 1 with probability 0.99.  Philox keyed by (seed, row).
-__global__ __launch_bounds__(256) void fill_kernel(float* data, int rec, int sd, int ad,
-                                                   int64_t start, int64_t n, int64_t cap,
+__global__ __launch_bounds__(256) void fill_kernel(float* data, int rec, int o_a, int ad, int o_r,
+                                                   int o_nd, int64_t start, int64_t n, int64_t cap,
                                                    float max_action, uint64_t seed) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
   const int64_t slot = (start + i) % cap;
   float* r = data + (size_t)slot * rec;
-  const int nf = 2 * sd + ad + 2;
   for (int c0 = lane * 4; c0 < rec; c0 += 256) {
     float z[4];
     philox_normal4(seed, (uint64_t)i, kStreamFill, (uint32_t)c0, z);
@@ -80,15 +97,15 @@ __global__ __launch_bounds__(256) void fill_kernel(float* data, int rec, int sd,
       const int c = c0 + j;
       if (c >= rec) break;
       float v;
-      if (c >= nf) v = 0.f;
-      else if (c < sd) v = z[j];
-      else if (c < sd + ad) v = max_action * (2.f * ((float)(uu[j] >> 8) * (1.f / 16777216.f)) - 1.f);
-      else if (c < 2 * sd + ad) v = z[j];
-      else if (c == 2 * sd + ad) v = z[j];
-      else v = ((float)(uu[j] >> 8) * (1.f / 16777216.f)) < 0.01f ? 0.f : 1.f;
+      if (c > o_nd) v = 0.f;                                            // record pad
+      else if (c == o_nd) v = ((float)(uu[j] >> 8) * (1.f / 16777216.f)) < 0.01f ? 0.f : 1.f;
+      else if (c >= o_a && c < o_a + ad)
+        v = max_action * (2.f * ((float)(uu[j] >> 8) * (1.f / 16777216.f)) - 1.f);
+      else v = z[j];                                                    // states, particles, reward
       r[c] = v;
     }
   }
+  (void)o_r;
 }
 
 __global__ void set_i64_kernel(int64_t* p, int64_t v) { *p = v; }
@@ -100,22 +117,7 @@ using namespace td3;
 // ================================================================== C-ABI
 extern "C" {
 
-int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint64_t seed,
-              rb_handle** out) {
-  TD3_ARG(out != nullptr, "out is null");
-  TD3_ARG(state_dim > 0 && action_dim > 0, "dims must be positive");
-  TD3_ARG(pad4(2 * state_dim + action_dim + 2) <= kMaxRecord, "record too wide");
-  TD3_ARG(max_size > 0, "max_size must be positive");
-  TD3_HIP(hipSetDevice(device));
-  Ring* r = new Ring();
-  r->sd = state_dim;
-  r->ad = action_dim;
-  r->o_s = 0;
-  r->o_a = state_dim;
-  r->o_s2 = state_dim + action_dim;
-  r->o_r = 2 * state_dim + action_dim;
-  r->o_nd = r->o_r + 1;
-  r->rec = pad4(2 * state_dim + action_dim + 2);
+static int ring_alloc(Ring* r, int64_t max_size, int device, uint64_t seed, rb_handle** out) {
   r->cap = max_size;
   r->seed = seed;
   r->device = device;
@@ -133,6 +135,49 @@ int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint6
   TD3_HIP(hipEventCreateWithFlags(&r->stage_ev, hipEventDisableTiming));
   *out = reinterpret_cast<rb_handle*>(r);
   return 0;
+}
+
+int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint64_t seed,
+              rb_handle** out) {
+  TD3_ARG(out != nullptr, "out is null");
+  TD3_ARG(state_dim > 0 && action_dim > 0, "dims must be positive");
+  TD3_ARG(pad4(2 * state_dim + action_dim + 2) <= kMaxRecord, "record too wide");
+  TD3_ARG(max_size > 0, "max_size must be positive");
+  TD3_HIP(hipSetDevice(device));
+  Ring* r = new Ring();
+  r->sd = state_dim;
+  r->ad = action_dim;
+  r->o_s = 0;
+  r->o_a = state_dim;
+  r->o_s2 = state_dim + action_dim;
+  r->o_r = 2 * state_dim + action_dim;
+  r->o_nd = r->o_r + 1;
+  r->rec = pad4(2 * state_dim + action_dim + 2);
+  return ring_alloc(r, max_size, device, seed, out);
+}
+
+int rb_create_particles(int feat_dim, int n_particles, int particle_dim, int action_dim, int64_t max_size,
+                        int device, uint64_t seed, rb_handle** out) {
+  TD3_ARG(out != nullptr, "out is null");
+  TD3_ARG(feat_dim > 0 && n_particles > 0 && particle_dim > 0 && action_dim > 0, "dims must be positive");
+  TD3_ARG(max_size > 0, "max_size must be positive");
+  TD3_HIP(hipSetDevice(device));
+  Ring* r = new Ring();
+  const int np = n_particles * particle_dim;
+  r->particles = 1;
+  r->N = n_particles;
+  r->D = particle_dim;
+  r->sd = feat_dim;
+  r->ad = action_dim;
+  r->o_s = 0;
+  r->o_p = feat_dim;
+  r->o_a = feat_dim + np;
+  r->o_s2 = r->o_a + action_dim;
+  r->o_p2 = r->o_s2 + feat_dim;
+  r->o_r = r->o_p2 + np;
+  r->o_nd = r->o_r + 1;
+  r->rec = pad4(r->o_nd + 1);
+  return ring_alloc(r, max_size, device, seed, out);
 }
 
 int rb_destroy(rb_handle* h) {
@@ -161,6 +206,8 @@ int rb_info(const rb_handle* h, rb_info_t* info) {
   info->size = r->size;
   info->data = r->data;
   info->device = r->device;
+  info->n_particles = r->N;
+  info->particle_dim = r->D;
   return 0;
 }
 
@@ -210,6 +257,7 @@ int rb_add(rb_handle* h, const double* state, const double* action, const double
   if (n == 0) return 0;
   TD3_ARG(state && action && next_state && reward && done, "null input");
   Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_ARG(!r->particles, "rb_add on a particle ring (use rb_add_particles)");
   TD3_HIP(hipSetDevice(r->device));
   int rc = ensure_stage(r, (size_t)n * r->rec);
   if (rc) return rc;
@@ -220,6 +268,34 @@ int rb_add(rb_handle* h, const double* state, const double* action, const double
     for (int c = 0; c < r->sd; ++c) d[r->o_s2 + c] = (float)next_state[i * r->sd + c];
     d[r->o_r] = (float)reward[i];
     d[r->o_nd] = (float)(1.0 - done[i]);                  // my_replay_buffer.py:114
+    for (int c = r->o_nd + 1; c < r->rec; ++c) d[c] = 0.f;
+  }
+  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
+  return push_staged(r, r->stage, n, s);
+}
+
+int rb_add_particles(rb_handle* h, const double* feat, const double* part, const double* action,
+                     const double* next_feat, const double* next_part, const double* reward,
+                     const double* done, int64_t n, void* stream) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(n >= 0, "n must be >= 0");
+  if (n == 0) return 0;
+  TD3_ARG(feat && part && action && next_feat && next_part && reward && done, "null input");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_ARG(r->particles, "rb_add_particles on a featured ring");
+  TD3_HIP(hipSetDevice(r->device));
+  int rc = ensure_stage(r, (size_t)n * r->rec);
+  if (rc) return rc;
+  const int np = r->N * r->D;
+  for (int64_t i = 0; i < n; ++i) {                        // my_replay_buffer.py:46-56
+    float* d = r->stage + (size_t)i * r->rec;
+    for (int c = 0; c < r->sd; ++c) d[r->o_s + c] = (float)feat[i * r->sd + c];
+    for (int c = 0; c < np; ++c) d[r->o_p + c] = (float)part[i * np + c];
+    for (int c = 0; c < r->ad; ++c) d[r->o_a + c] = (float)action[i * r->ad + c];
+    for (int c = 0; c < r->sd; ++c) d[r->o_s2 + c] = (float)next_feat[i * r->sd + c];
+    for (int c = 0; c < np; ++c) d[r->o_p2 + c] = (float)next_part[i * np + c];
+    d[r->o_r] = (float)reward[i];
+    d[r->o_nd] = (float)(1.0 - done[i]);
     for (int c = r->o_nd + 1; c < r->rec; ++c) d[c] = 0.f;
   }
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
@@ -249,8 +325,8 @@ int rb_fill_synthetic(rb_handle* h, int64_t n, float max_action, uint64_t seed, 
   if (n > r->cap) n = r->cap;
   if (n > 0) {
     dim3 grid((unsigned)((n + 3) / 4));
-    hipLaunchKernelGGL(fill_kernel, grid, dim3(256), 0, s, r->data, r->rec, r->sd, r->ad, r->ptr,
-                       n, r->cap, max_action, seed);
+    hipLaunchKernelGGL(fill_kernel, grid, dim3(256), 0, s, r->data, r->rec, r->o_a, r->ad, r->o_r, r->o_nd,
+                       r->ptr, n, r->cap, max_action, seed);
     TD3_HIP(hipGetLastError());
   }
   r->ptr = (r->ptr + n) % r->cap;
@@ -266,6 +342,7 @@ int rb_sample(rb_handle* h, int batch, float* state, float* action, float* next_
               void* stream) {
   TD3_ARG(h != nullptr, "null handle");
   Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_ARG(!r->particles, "rb_sample on a particle ring (use rb_sample_particles)");
   TD3_ARG(batch >= 0, "batch must be >= 0");
   TD3_ARG(r->size > 0 || batch == 0 || inject_idx, "sample from an empty buffer");
   TD3_ARG(state && action && next_state && reward && not_done, "null output");
@@ -288,6 +365,40 @@ int rb_sample(rb_handle* h, int batch, float* state, float* action, float* next_
   a.step = ++r->sample_calls;
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
   TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));   // add() before sample() (main.py:261, :269)
+  return launch_gather(a, s);
+}
+
+int rb_sample_particles(rb_handle* h, int batch, float* feat, float* part, float* action, float* next_feat,
+                        float* next_part, float* reward, float* not_done, const int64_t* inject_idx,
+                        int64_t* idx_out, void* stream) {
+  TD3_ARG(h != nullptr, "null handle");
+  Ring* r = reinterpret_cast<Ring*>(h);
+  TD3_ARG(r->particles, "rb_sample_particles on a featured ring");
+  TD3_ARG(batch >= 0, "batch must be >= 0");
+  TD3_ARG(r->size > 0 || batch == 0 || inject_idx, "sample from an empty buffer");
+  TD3_ARG(feat && part && action && next_feat && next_part && reward && not_done, "null output");
+  TD3_HIP(hipSetDevice(r->device));
+  const int np = r->N * r->D;
+  GatherArgs a{};
+  a.seg[0] = GatherSeg{feat, r->sd, 0, r->o_s, r->sd};
+  a.seg[1] = GatherSeg{part, np, 0, r->o_p, np};
+  a.seg[2] = GatherSeg{action, r->ad, 0, r->o_a, r->ad};
+  a.seg[3] = GatherSeg{next_feat, r->sd, 0, r->o_s2, r->sd};
+  a.seg[4] = GatherSeg{next_part, np, 0, r->o_p2, np};
+  a.seg[5] = GatherSeg{reward, 1, 0, r->o_r, 1};
+  a.seg[6] = GatherSeg{not_done, 1, 0, r->o_nd, 1};
+  a.nseg = 7;
+  a.B = a.Bp = batch;
+  a.data = r->data;
+  a.rec = r->rec;
+  a.d_size = r->d_size;
+  a.inject_idx = inject_idx;
+  a.idx_out = idx_out;
+  a.seed = r->seed;
+  a.ctr = nullptr;
+  a.step = ++r->sample_calls;
+  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
+  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
   return launch_gather(a, s);
 }
 

@@ -26,6 +26,7 @@
 #include <string>
 #include <vector>
 
+#include "encoder.h"
 #include "kernels.h"
 #include "replay.h"
 #include "../../include/td3.h"
@@ -53,6 +54,12 @@ struct LNormL { int N, Np; int64_t offg, offb; };
 struct NetL {
   LinearL lin[4];
   LNormL ln[3];
+  // TD3_particles networks: the particle encoder block (EncOff layout) and lnorm1, the
+  // LayerNorm of the concatenated MLP input (TD3_particles.py:43-46 / :95-98)
+  int D = 0;                 // particle feature width (0: featured network)
+  int64_t enc_off = -1;
+  bool lnin = false;
+  LNormL ln_in{};
 };
 struct TensorRef { std::string name; int64_t rows, cols; int64_t off; int ld; };
 
@@ -63,9 +70,23 @@ struct Group {
   std::vector<TensorRef> tensors;
 };
 
+// Parameter layout of one network in reference state_dict order.  Featured (TD3_featured.py:
+// 15-37 / 50-71): linears.{0..3}, lnorms.{0..2}.  Particles (TD3_particles.py:19-50 / 71-101):
+// conv1, conv2, linears.{0..3}, lnorm1, lnorms.{0..2}.
 static NetL layout_mlp(int in, const int hid[3], int out, bool norm, const std::string& prefix,
-                       int64_t& off, std::vector<TensorRef>& tensors) {
+                       int64_t& off, std::vector<TensorRef>& tensors, int enc_D = 0) {
   NetL n{};
+  if (enc_D > 0) {
+    off = (off + 3) & ~(int64_t)3;           // float4 loads of the conv2 weight
+    n.D = enc_D;
+    n.enc_off = off;
+    tensors.push_back({prefix + "conv1.weight", kEncC1, enc_D, off + EncOff::w1(enc_D), enc_D});
+    tensors.push_back({prefix + "conv1.bias", kEncC1, 0, off + EncOff::b1(enc_D), 0});
+    tensors.push_back({prefix + "conv2.weight", kEncC2, kEncC1, off + EncOff::w2(enc_D), kEncC1});
+    tensors.push_back({prefix + "conv2.bias", kEncC2, 0, off + EncOff::b2(enc_D), 0});
+    off += EncOff::size(enc_D);
+    off = (off + 31) & ~(int64_t)31;
+  }
   int dims[5] = {in, hid[0], hid[1], hid[2], out};
   for (int l = 0; l < 4; ++l) {
     LinearL& L = n.lin[l];
@@ -79,6 +100,19 @@ static NetL layout_mlp(int in, const int hid[3], int out, bool norm, const std::
     off += L.Np;
     tensors.push_back({prefix + "linears." + std::to_string(l) + ".weight", L.N, L.K, L.offW, L.Kp});
     tensors.push_back({prefix + "linears." + std::to_string(l) + ".bias", L.N, 0, L.offb, 0});
+  }
+  if (enc_D > 0) {
+    n.lnin = norm;
+    n.ln_in.N = in;
+    n.ln_in.Np = pad32(in);
+    n.ln_in.offg = off;
+    off += n.ln_in.Np;
+    n.ln_in.offb = off;
+    off += n.ln_in.Np;
+    if (norm) {
+      tensors.push_back({prefix + "lnorm1.weight", in, 0, n.ln_in.offg, 0});
+      tensors.push_back({prefix + "lnorm1.bias", in, 0, n.ln_in.offb, 0});
+    }
   }
   for (int l = 0; l < 3; ++l) {
     LNormL& Ln = n.ln[l];
@@ -105,7 +139,13 @@ struct EvalB {
   float* GU[3] = {};
   float* GZ[4] = {};
   float* T = nullptr;   // policy head tanh output [Bp][32]
-  float* Qv = nullptr;  // [Bp]
+  float* Qv = nullptr;  // [Bp] (featured) / [Bp][32] (particles: one Q per action dim)
+  // particles: lnorm1 output / stats / grad, conv2 ReLU bits, encoder grad partial slabs
+  float* Uin = nullptr;
+  float* statsIn = nullptr;
+  float* GUin = nullptr;
+  uint64_t* mask = nullptr;
+  float* partial = nullptr;
 };
 
 struct Scratch {
@@ -145,12 +185,26 @@ struct Plan {
   // the same bodies with the replay-ring gather captured in front (Philox draw path)
   hipGraphExec_t graph_g[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   const void* graph_ring = nullptr;
+  // ---- TD3_particles
+  int particles = 0;
+  int nq = 1, ldq = 1;                  // Q outputs per row and the row stride of Y / Qv
+  int ld_a = 0, ld_q = 0;               // MLP input widths (pad32(128+F), pad32(128+F+A))
+  float *XA = nullptr, *XTA = nullptr, *XAQ = nullptr, *XQ[2] = {}, *XTQ[2] = {};
+  float* pbatch = nullptr;              // foreign-buffer path: [Bp][2*N*D] particles of (s, s')
+  int64_t* d_iota = nullptr;
+  const float* src_data = nullptr;      // where the encoders read particles: ring or pbatch
+  int src_rec = 0, src_op = 0, src_op2 = 0;
+  const int64_t* src_idx = nullptr;
+  const void* src_key = nullptr;
+  int nwg = 0;                          // encoder-backward workgroups per role per network
 };
 
 struct ActPlan {       // select_action / eval_q at small batch
   int Bp = 0;
   float* scratch = nullptr;
   float *X_S = nullptr, *X_SA = nullptr, *X_SP = nullptr;
+  float *XQ2 = nullptr, *pbatch = nullptr, *out = nullptr;   // particles
+  int64_t* d_iota = nullptr;
   EvalB A, Q[2];
   std::vector<void*> tables;
   std::vector<Stage> act, evalq;
@@ -162,7 +216,8 @@ using namespace td3;
 
 struct td3_handle {
   td3_config cfg;
-  int sd, ad;
+  int sd, ad;                 // featured: state / action dims; particles: feature / action dims
+  int particles = 0, N = 0, D = 0, cdq = 1;
   Group actor, critic;
   float* arena = nullptr;
   Counters* d_ctr = nullptr;
@@ -206,7 +261,13 @@ static void alloc_eval(Scratch& S, const NetL& n, int Bp, float* X, int ldx, boo
   if (bwd) e.GZ[3] = S.take((size_t)Bp * 32);
   if (policy_or_q) {
     e.T = S.take((size_t)Bp * 32);
-    e.Qv = S.take((size_t)Bp);
+    e.Qv = S.take((size_t)Bp * 32);
+  }
+  if (n.D > 0) {
+    const int Kp0 = n.lin[0].Kp;
+    e.Uin = norm ? S.take((size_t)Bp * Kp0) : X;
+    e.statsIn = S.take((size_t)2 * Bp);
+    if (bwd) e.GUin = S.take((size_t)Bp * Kp0);
   }
 }
 
@@ -263,7 +324,8 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     int maxKp = 0;
     for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Kp);
     const int wn = maxKp <= 128 ? 4 : 1;
-    const int pro = l == 0 ? kProCopy : (norm ? kProLN : kProCopy);
+    const bool lnin = items[0].net->lnin;          // TD3_particles lnorm1 on the MLP input
+    const int pro = l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
     int blocks = 0, lds = 0;
     double flops = 0;
     for (size_t k = 0; k < items.size(); ++k) {
@@ -275,6 +337,15 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       if (l == 0) {
         p.A = it.e->X;
         p.lda = it.e->ldx;
+        if (lnin) {
+          p.lng = it.P + it.net->ln_in.offg;
+          p.lnb = it.P + it.net->ln_in.offb;
+          p.stats = it.stats ? it.e->statsIn : nullptr;
+          if (it.store_u) {
+            p.Aout = it.e->Uin;
+            p.ldao = L.Kp;
+          }
+        }
       } else {
         p.A = it.e->H[l - 1];
         p.lda = it.net->lin[l - 1].Np;
@@ -313,11 +384,13 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 
 // dU_1 = dZ_2 * W_2 (dZ_2 built by the fused head prologue `pro2`), dU_0 = dZ_1 * W_1
 // (dZ_1 = relu'(LN_bwd(dU_1)) in the prologue), then dZ_0 rows when needed.
+// need_in (TD3_particles): dU_in = dZ_0 * W_0 as well (dZ_0 formed in its prologue and kept),
+// the input grad that feeds lnorm1's backward, the encoder and dQ1/da; replaces the dZ_0 rows.
 static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<BwdItem>& items, int Bp, int B, const char* tag,
-                          bool need_dz0) {
+                          bool need_dz0, bool need_in = false) {
   const bool norm = h->cfg.norm != 0;
-  for (int l = 2; l >= 1; --l) {
+  for (int l = 2; l >= (need_in ? 0 : 1); --l) {
     std::vector<GemmProb> probs;
     int blocks = 0, lds = 0;
     double flops = 0;
@@ -334,14 +407,14 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
         p.A = it.e->GZ[2];
         p.lda = L.Np;
       } else {
-        p.A = it.e->GU[1];
+        p.A = it.e->GU[l];
         p.lda = L.Np;
-        p.H = it.e->H[1];
+        p.H = it.e->H[l];
         p.ldh = L.Np;
-        p.lng = it.P + it.net->ln[1].offg;
-        p.stats = it.e->stats[1];
+        p.lng = it.P + it.net->ln[l].offg;
+        p.stats = it.e->stats[l];
         if (it.store_dz) {
-          p.Aout = it.e->GZ[1];
+          p.Aout = it.e->GZ[l];
           p.ldao = L.Np;
         }
       }
@@ -350,7 +423,7 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.W = it.P + L.offW;
       p.ldw = L.Kp;
       p.Nout = L.Kp;
-      p.C = it.e->GU[l - 1];
+      p.C = l > 0 ? it.e->GU[l - 1] : it.e->GUin;
       p.ldc = L.Kp;
       p.relu = 0;
       p.ntiles = (L.Kp + 32 * wn - 1) / (32 * wn);
@@ -363,7 +436,7 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, l == 2 ? kProCopy : kProLNBwd, Bp, lds, blocks,
                            flops, std::string(tag) + "_bwd" + std::to_string(l), nullptr, 0));
   }
-  if (need_dz0) {
+  if (need_dz0 && !need_in) {
     std::vector<LnBwdProb> probs;
     for (auto& it : items) {
       const LinearL& L = it.net->lin[0];
@@ -390,9 +463,10 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 }
 
 // Weight / bias / LN grads of every layer of `items`, fused with the optimizer.
+// enc (TD3_particles): the encoder partial slabs of `items` (reduced + optimizer in one launch).
 static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                         Group& g, int which, const std::vector<BwdItem>& items, int Bp,
-                        const char* tag, bool polyak) {
+                        const char* tag, bool polyak, int enc_nwg = 0) {
   const bool norm = h->cfg.norm != 0;
   std::vector<DwProb> probs;
   int blocks = 0;
@@ -404,8 +478,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       DwProb p{};
       p.G = it.e->GZ[l];
       p.ldg = (l == 3) ? 32 : L.Np;
-      p.U = (l == 0) ? it.e->X : it.e->U[l - 1];
-      p.ldu = (l == 0) ? it.e->ldx : n.lin[l - 1].Np;
+      p.U = (l == 0) ? (n.D > 0 ? it.e->Uin : it.e->X) : it.e->U[l - 1];
+      p.ldu = (l == 0) ? ((n.D > 0 && norm) ? L.Kp : it.e->ldx) : n.lin[l - 1].Np;
       p.Np = L.Np;
       p.Kp = L.Kp;
       p.offW = L.offW;
@@ -426,6 +500,22 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       p.tile_begin = blocks;
       blocks += (L.Np / 32) * p.ntk + L.Np / 32;     // matrix tiles, then vector tiles
       flops += 2.0 * Bp * L.N * L.K;
+      probs.push_back(p);
+    }
+    if (n.lnin) {                                   // lnorm1 affine grads (vector tiles only)
+      DwProb p{};
+      p.Np = n.ln_in.Np;
+      p.offb = -1;
+      p.offg = n.ln_in.offg;
+      p.offbeta = n.ln_in.offb;
+      p.GU = it.e->GUin;
+      p.ldgu = n.lin[0].Kp;
+      p.H = it.e->X;
+      p.ldh = it.e->ldx;
+      p.stats = it.e->statsIn;
+      p.ntk = 0;
+      p.tile_begin = blocks;
+      blocks += p.Np / 32;
       probs.push_back(p);
     }
   }
@@ -451,6 +541,22 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.mode = dp ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
   st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
                 "td3::dw_kernel"});
+  if (enc_nwg > 0) {
+    EncAdamArgs ea{};
+    for (auto& it : items) {
+      if (it.net->D <= 0) continue;
+      TD3_ARG(ea.nprob < 3, "too many encoders in one dw stage");
+      ea.p[ea.nprob].partial = it.e->partial;
+      ea.p[ea.nprob].off = it.net->enc_off;
+      ea.nprob++;
+    }
+    ea.nwg = enc_nwg;
+    ea.size = EncOff::size(items[0].net->D);
+    ea.adam = a.adam;
+    ea.mode = a.mode;
+    st.push_back({std::string(tag) + "_enc_adam", [=](hipStream_t s) { return launch_enc_adam(ea, s); }, 0,
+                  "td3::enc_adam_kernel"});
+  }
   if (dp) {
     ncclComm_t comm = h->comm;
     float* G = g.G;
@@ -494,6 +600,7 @@ static void destroy_plan(Plan* p) {
 
 static size_t eval_floats(const NetL& n, int Bp, bool bwd, bool norm) {
   size_t f = 0;
+  if (n.D > 0) f += (size_t)Bp * n.lin[0].Kp * 2 + 2 * (size_t)Bp + 256;
   for (int l = 0; l < 3; ++l) {
     size_t np = (size_t)Bp * n.lin[l].Np;
     f += np + 64;
@@ -501,7 +608,7 @@ static size_t eval_floats(const NetL& n, int Bp, bool bwd, bool norm) {
     f += 2 * (size_t)Bp + 64;
     if (bwd) f += 2 * (np + 64);
   }
-  f += (size_t)Bp * 32 * 2 + Bp + 256;
+  f += (size_t)Bp * 32 * 3 + 256;
   return f;
 }
 
@@ -583,6 +690,7 @@ static int build_step(td3_handle* h, int B) {
     p.exi[6] = sd;
     p.exi[7] = ad;
     p.exi[8] = target;
+    p.exi[9] = 1;                                  // clamp a' to +-max_action (TD3_featured.py:135-137)
     p.exf[0] = ma;
     p.exf[1] = (float)h->cfg.policy_noise;
     p.exf[2] = (float)h->cfg.noise_clip;
@@ -718,13 +826,370 @@ static int build_step(td3_handle* h, int B) {
   return 0;
 }
 
+// ================================================================== TD3_particles step
+// TD3_particles.TD3.train (TD3_particles.py:167-224): the featured schedule plus the particle
+// encoder of every network (enc_fwd / enc_bwd / enc_adam), lnorm1 on the MLP input, Q heads with
+// one output per action dimension, no clamp on a', tanh policy output, optional CDQ.
+struct EncItem {
+  const NetL* net;
+  const float* P;         // group arena (encoder at P + net->enc_off)
+  float* X; int ldx;      // pooled features -> X[:, 0:128]
+  int next;               // 1: the next-state particles
+  uint64_t* mask;         // nullable (networks that are back-propagated)
+};
+
+static void push_enc_fwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const std::vector<EncItem>& items,
+                         const std::string& name) {
+  const int N = h->N, D = h->D;
+  const double flops = 2.0 * P->B * N * ((double)kEncC1 * D + (double)kEncC2 * kEncC1) * items.size();
+  st.push_back({name,
+                [=](hipStream_t s) {
+                  EncFwdArgs a{};
+                  for (size_t k = 0; k < items.size(); ++k) {
+                    const EncItem& it = items[k];
+                    a.p[k] = EncFwdProb{it.P + it.net->enc_off, it.next ? P->src_op2 : P->src_op, it.X, it.ldx,
+                                        it.mask};
+                  }
+                  a.nprob = (int)items.size();
+                  a.data = P->src_data;
+                  a.rec = P->src_rec;
+                  a.idx = P->src_idx;
+                  a.B = P->B;
+                  a.Bp = P->Bp;
+                  a.N = N;
+                  a.D = D;
+                  a.ntile = (N + 31) / 32;
+                  return launch_enc_fwd(a, s);
+                },
+                flops, "td3::enc_fwd_kernel<" + std::to_string(((D + 3) / 4) * 4) + ">"});
+}
+
+static void push_enc_bwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const std::vector<BwdItem>& items,
+                         const std::vector<float*>& X, const std::string& name) {
+  const int N = h->N, D = h->D;
+  const bool norm = h->cfg.norm != 0;
+  const double flops = 2.0 * P->B * N * (2.0 * kEncC2 * kEncC1 + (double)kEncC1 * D) * items.size();
+  st.push_back({name,
+                [=](hipStream_t s) {
+                  EncBwdArgs a{};
+                  for (size_t k = 0; k < items.size(); ++k) {
+                    const BwdItem& it = items[k];
+                    EncBwdProb& q = a.p[k];
+                    q.enc = it.P + it.net->enc_off;
+                    q.part_off = P->src_op;
+                    q.mask = it.e->mask;
+                    q.X = X[k];
+                    q.ldx = it.net->lin[0].Kp;
+                    q.GU = it.e->GUin;
+                    q.ldgu = it.net->lin[0].Kp;
+                    q.stats = norm ? it.e->statsIn : nullptr;
+                    q.gamma = it.P + it.net->ln_in.offg;
+                    q.Kin = it.net->lin[0].K;
+                    q.partial = it.e->partial;
+                  }
+                  a.nprob = (int)items.size();
+                  a.data = P->src_data;
+                  a.rec = P->src_rec;
+                  a.idx = P->src_idx;
+                  a.B = P->B;
+                  a.Bp = P->Bp;
+                  a.N = N;
+                  a.D = D;
+                  a.ntile = (N + 31) / 32;
+                  a.nwg = P->nwg;
+                  return launch_enc_bwd(a, s);
+                },
+                flops, "td3::enc_bwd_kernel<" + std::to_string(((D + 3) / 4) * 4) + ", 0>"});
+}
+
+static void destroy_graphs(Plan* P) {
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      if (P->graph[a][b]) hipGraphExecDestroy(P->graph[a][b]);
+      if (P->graph_g[a][b]) hipGraphExecDestroy(P->graph_g[a][b]);
+      P->graph[a][b] = P->graph_g[a][b] = nullptr;
+    }
+  P->graph_ring = nullptr;
+}
+
+// The encoders read particles in place; graphs bake the source, so a new source re-captures.
+static void set_particle_source(Plan* P, const void* key, const float* data, int rec, int op, int op2,
+                                const int64_t* idx) {
+  if (P->src_key == key && P->src_data == data) return;
+  destroy_graphs(P);
+  P->src_key = key;
+  P->src_data = data;
+  P->src_rec = rec;
+  P->src_op = op;
+  P->src_op2 = op2;
+  P->src_idx = idx;
+}
+
+static int build_step_particles(td3_handle* h, int B) {
+  std::unique_ptr<Plan> P(new Plan());
+  const int Bp = pad32(B);
+  P->B = B;
+  P->Bp = Bp;
+  P->particles = 1;
+  const bool norm = h->cfg.norm != 0;
+  const bool cdq = h->cdq != 0;
+  const int F = h->sd, ad = h->ad, N = h->N, D = h->D;
+  const int nqn = cdq ? 2 : 1;
+  const NetL& an = h->actor.nets[0];
+  const NetL& q1 = h->critic.nets[0];
+  const NetL& q2 = h->critic.nets[cdq ? 1 : 0];
+  P->nq = ad;
+  P->ldq = 32;
+  P->ld_a = an.lin[0].Kp;
+  P->ld_q = q1.lin[0].Kp;
+  P->nwg = std::max(1, std::min(B, 256 / nqn));
+  const int ntile = (N + 31) / 32;
+  const size_t encsz = (size_t)EncOff::size(D);
+  const size_t mask_f = (size_t)Bp * ntile * 64 * 2;
+  size_t floats = (size_t)Bp * (2 * P->ld_a + 5 * P->ld_q) + 16 * (size_t)Bp + (size_t)Bp * ad +
+                  (size_t)Bp * 32 + (size_t)Bp * 2 * N * D + 3 * mask_f + 3 * P->nwg * encsz + 16384;
+  floats += 2 * eval_floats(an, Bp, true, norm) + 6 * eval_floats(q1, Bp, true, norm);
+  P->scratch_bytes = floats * sizeof(float);
+  TD3_HIP(hipMalloc(&P->scratch, P->scratch_bytes));
+  TD3_HIP(hipMemset(P->scratch, 0, P->scratch_bytes));
+  Scratch S{P->scratch, floats, 0};
+  P->XA = S.take((size_t)Bp * P->ld_a);
+  P->XTA = S.take((size_t)Bp * P->ld_a);
+  P->XAQ = S.take((size_t)Bp * P->ld_q);
+  for (int j = 0; j < nqn; ++j) {
+    P->XQ[j] = S.take((size_t)Bp * P->ld_q);
+    P->XTQ[j] = S.take((size_t)Bp * P->ld_q);
+  }
+  P->R = S.take(Bp);
+  P->ND = S.take(Bp);
+  P->noise = S.take((size_t)Bp * ad);
+  P->Y = S.take((size_t)Bp * 32);
+  P->sqerr = S.take(2 * (size_t)Bp);
+  P->d_idx = (int64_t*)S.take(2 * (size_t)Bp);
+  P->d_inject_idx = (int64_t*)S.take(2 * (size_t)Bp);
+  P->d_iota = (int64_t*)S.take(2 * (size_t)Bp);
+  P->pbatch = S.take((size_t)Bp * 2 * N * D);
+  alloc_eval(S, an, Bp, P->XTA, P->ld_a, false, norm, true, P->TA);
+  alloc_eval(S, an, Bp, P->XA, P->ld_a, true, norm, true, P->A);
+  for (int j = 0; j < nqn; ++j) {
+    alloc_eval(S, j ? q2 : q1, Bp, P->XQ[j], P->ld_q, true, norm, true, P->Q[j]);
+    alloc_eval(S, j ? q2 : q1, Bp, P->XTQ[j], P->ld_q, false, norm, true, P->TQ[j]);
+  }
+  alloc_eval(S, q1, Bp, P->XAQ, P->ld_q, true, norm, true, P->AQ);
+  for (EvalB* e : {&P->Q[0], &P->Q[1], &P->A}) {
+    if (e == &P->Q[1] && !cdq) continue;
+    e->mask = reinterpret_cast<uint64_t*>(S.take(mask_f));
+    e->partial = S.take((size_t)P->nwg * encsz);
+  }
+  if (S.used > S.cap) {
+    set_error("internal: scratch overflow (%zu > %zu)", S.used, S.cap);
+    return -2;
+  }
+  {
+    std::vector<int64_t> iota(Bp);
+    for (int i = 0; i < Bp; ++i) iota[i] = i;
+    TD3_HIP(hipMemcpy(P->d_iota, iota.data(), Bp * 8, hipMemcpyHostToDevice));
+  }
+
+  const float* Pa = h->actor.P;
+  const float* Pta = h->actor.T;
+  const float* Pq = h->critic.P;
+  const float* Ptq = h->critic.T;
+  const int acol = kEncC2 + F;        // first action column of the Q input rows (TD3_particles.py:110)
+
+  auto policy_head = [&](const float* Pp, EvalB& e, float* out, float* out2, int target, int gen_noise) {
+    GemmProb p{};
+    p.norm = norm ? 1 : 0;
+    p.B = B;
+    p.ex[0] = e.H[2];
+    p.ex[1] = const_cast<float*>(Pp + an.ln[2].offg);
+    p.ex[2] = const_cast<float*>(Pp + an.ln[2].offb);
+    p.ex[3] = const_cast<float*>(Pp + an.lin[3].offW);
+    p.ex[4] = const_cast<float*>(Pp + an.lin[3].offb);
+    p.ex[5] = P->noise;
+    p.ex[6] = out;
+    p.ex[7] = e.T;
+    p.ex[8] = e.U[2];
+    p.ex[9] = e.stats[2];
+    p.ex[10] = out2;
+    p.exi[0] = an.lin[2].N;
+    p.exi[1] = an.lin[2].Np;
+    p.exi[2] = an.lin[3].Kp;
+    p.exi[3] = P->ld_q;
+    p.exi[4] = gen_noise;
+    p.exi[5] = ad;
+    p.exi[6] = acol;
+    p.exi[7] = ad;
+    p.exi[8] = target;
+    p.exi[9] = 0;                                  // no clamp of a' (TD3_particles.py:179-181)
+    p.exf[0] = 1.0f;                               // tanh output (:68)
+    p.exf[1] = (float)h->cfg.policy_noise;
+    p.exf[2] = (float)h->cfg.noise_clip;
+    p.seed = h->cfg.seed;
+    p.ctr = h->d_ctr;
+    return p;
+  };
+
+  for (int actor_phase = 0; actor_phase < 2; ++actor_phase) {
+    for (int inj = 0; inj < 2; ++inj) {
+      std::vector<Stage>& st = P->body[actor_phase][inj];
+      Plan* Pp = P.get();
+      // ---- encoders of the critic phase (+ the actor's on policy steps)
+      {
+        std::vector<EncItem> e = {{&an, Pta, P->XTA, P->ld_a, 1, nullptr},
+                                  {&q1, Ptq, P->XTQ[0], P->ld_q, 1, nullptr},
+                                  {&q1, Pq, P->XQ[0], P->ld_q, 0, P->Q[0].mask}};
+        if (cdq) {
+          e.push_back({&q2, Ptq, P->XTQ[1], P->ld_q, 1, nullptr});
+          e.push_back({&q2, Pq, P->XQ[1], P->ld_q, 0, P->Q[1].mask});
+        }
+        if (actor_phase) e.push_back({&an, Pa, P->XA, P->ld_a, 0, P->A.mask});
+        push_enc_fwd(h, Pp, st, e, "ENC_fwd");
+      }
+      std::vector<FwdItem> f1 = {{&an, Pta, &P->TA, false, false}, {&q1, Pq, &P->Q[0], true, true}};
+      if (cdq) f1.push_back({&q2, Pq, &P->Q[1], true, true});
+      if (actor_phase) f1.push_back({&an, Pa, &P->A, true, true});
+      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase));
+      {
+        std::vector<GemmProb> hp = {policy_head(Pta, P->TA, P->XTQ[0], cdq ? P->XTQ[1] : nullptr, 1, inj ? 0 : 1)};
+        if (actor_phase) hp.push_back(policy_head(Pa, P->A, P->XAQ, nullptr, 0, 0));
+        TD3_RC(push_row_stage(h, P->tables, st, hp, kRowPolicyHead, Bp, "heads"));
+      }
+      std::vector<FwdItem> f2 = {{&q1, Ptq, &P->TQ[0], false, false}};
+      if (cdq) f2.push_back({&q2, Ptq, &P->TQ[1], false, false});
+      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0));
+      {
+        std::vector<GemmProb> cl;
+        for (int j = 0; j < nqn; ++j) {
+          const NetL& qj = j ? q2 : q1;
+          const NetL& t1 = cdq ? q2 : q1;
+          EvalB& T1 = P->TQ[cdq ? 1 : 0];
+          GemmProb p{};
+          p.norm = norm ? 1 : 0;
+          p.B = B;
+          p.ex[0] = P->TQ[0].H[2];
+          p.ex[1] = T1.H[2];
+          p.ex[2] = P->Q[j].H[2];
+          p.ex[3] = const_cast<float*>(Ptq + q1.ln[2].offg);
+          p.ex[4] = const_cast<float*>(Ptq + t1.ln[2].offg);
+          p.ex[5] = const_cast<float*>(Pq + qj.ln[2].offg);
+          p.ex[6] = const_cast<float*>(Ptq + q1.ln[2].offb);
+          p.ex[7] = const_cast<float*>(Ptq + t1.ln[2].offb);
+          p.ex[8] = const_cast<float*>(Pq + qj.ln[2].offb);
+          p.ex[9] = const_cast<float*>(Ptq + q1.lin[3].offW);
+          p.ex[10] = const_cast<float*>(Ptq + t1.lin[3].offW);
+          p.ex[11] = const_cast<float*>(Pq + qj.lin[3].offW);
+          p.ex[12] = const_cast<float*>(Ptq + q1.lin[3].offb);
+          p.ex[13] = const_cast<float*>(Ptq + t1.lin[3].offb);
+          p.ex[14] = const_cast<float*>(Pq + qj.lin[3].offb);
+          p.ex[15] = P->R;
+          p.ex[16] = P->ND;
+          p.ex[17] = P->Q[j].GZ[3];
+          p.ex[18] = P->Q[j].GU[2];
+          p.ex[19] = P->Q[j].U[2];
+          p.ex[20] = P->Q[j].stats[2];
+          p.ex[21] = P->Y;
+          p.ex[22] = P->sqerr + (size_t)j * Bp;
+          p.ex[23] = P->Q[j].Qv;
+          p.Aout = P->Q[j].GZ[2];
+          p.ldao = qj.lin[2].Np;
+          p.exi[0] = qj.lin[2].N;
+          p.exi[1] = qj.lin[2].Np;
+          p.exi[2] = j;
+          p.exi[3] = ad;
+          p.exi[4] = qj.lin[3].Kp;
+          p.exi[5] = cdq ? 1 : 0;
+          p.exf[0] = (float)h->cfg.discount;
+          p.exf[1] = (float)(2.0 / ((double)B * ad));
+          cl.push_back(p);
+        }
+        TD3_RC(push_row_stage(h, P->tables, st, cl, kRowCriticLossP, Bp, "critic_loss"));
+      }
+      std::vector<BwdItem> cb = {{&q1, Pq, &P->Q[0], true}};
+      std::vector<float*> cbx = {P->XQ[0]};
+      if (cdq) {
+        cb.push_back({&q2, Pq, &P->Q[1], true});
+        cbx.push_back(P->XQ[1]);
+      }
+      TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true, true));
+      push_enc_bwd(h, Pp, st, cb, cbx, "CB_enc");
+      TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, P->nwg));
+      if (!actor_phase) continue;
+      // ---------------- delayed policy update (TD3_particles.py:206-224)
+      push_enc_fwd(h, Pp, st, {{&q1, Pq, P->XAQ, P->ld_q, 0, nullptr}}, "AF_enc");
+      std::vector<FwdItem> f3 = {{&q1, Pq, &P->AQ, false, true}};
+      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0));
+      {
+        GemmProb p{};
+        p.norm = norm ? 1 : 0;
+        p.B = B;
+        p.ex[0] = P->AQ.H[2];
+        p.ex[1] = const_cast<float*>(Pq + q1.ln[2].offg);
+        p.ex[2] = const_cast<float*>(Pq + q1.ln[2].offb);
+        p.ex[3] = const_cast<float*>(Pq + q1.lin[3].offW);
+        p.ex[4] = const_cast<float*>(Pq + q1.lin[3].offb);
+        p.ex[5] = P->AQ.Qv;
+        p.Aout = P->AQ.GZ[2];
+        p.ldao = q1.lin[2].Np;
+        p.exi[0] = q1.lin[2].N;
+        p.exi[1] = q1.lin[2].Np;
+        p.exi[2] = ad;
+        p.exi[3] = q1.lin[3].Kp;
+        p.exf[0] = (float)(-1.0 / ((double)B * ad));
+        std::vector<GemmProb> v = {p};
+        TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorLossP, Bp, "actor_loss"));
+      }
+      std::vector<BwdItem> aqb = {{&q1, Pq, &P->AQ, false}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false, true));
+      {
+        GemmProb p{};
+        p.norm = norm ? 1 : 0;
+        p.B = B;
+        p.ex[0] = P->AQ.GUin;
+        p.ex[1] = P->XAQ;
+        p.ex[2] = P->AQ.statsIn;
+        p.ex[3] = const_cast<float*>(Pq + q1.ln_in.offg);
+        p.ex[5] = P->A.T;
+        p.ex[6] = const_cast<float*>(Pa + an.lin[3].offW);
+        p.ex[7] = P->A.H[2];
+        p.ex[8] = P->A.stats[2];
+        p.ex[9] = const_cast<float*>(Pa + an.ln[2].offg);
+        p.ex[10] = P->A.GZ[3];
+        p.ex[11] = P->A.GU[2];
+        p.Aout = P->A.GZ[2];
+        p.ldao = an.lin[2].Np;
+        p.exi[0] = q1.lin[0].K;
+        p.exi[1] = q1.lin[0].Kp;
+        p.exi[3] = acol;
+        p.exi[4] = ad;
+        p.exi[5] = an.lin[2].N;
+        p.exi[6] = an.lin[2].Np;
+        p.exi[7] = an.lin[3].Kp;
+        p.exf[0] = 1.0f;
+        std::vector<GemmProb> v = {p};
+        TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorHeadBwdP, Bp, "actor_head_bwd"));
+      }
+      std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
+      TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true, true));
+      push_enc_bwd(h, Pp, st, ab, {P->XA}, "AB_enc");
+      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, P->nwg));
+    }
+  }
+  if (h->plan) destroy_plan(h->plan.get());
+  h->plan = std::move(P);
+  return 0;
+}
+
 static int run_stages(std::vector<Stage>& st, hipStream_t s) {
   for (auto& x : st) TD3_RC(x.run(s));
   return 0;
 }
 
 // Input stage: Philox index draw + gather from the ring into the padded batch buffers.
+static int input_from_ring_particles(td3_handle* h, Ring* r, Plan* P, bool inject_idx, hipStream_t s);
+
 static int input_from_ring(td3_handle* h, Ring* r, Plan* P, bool inject_idx, hipStream_t s) {
+  if (P->particles) return input_from_ring_particles(h, r, P, inject_idx, s);
   GatherArgs a{};
   const int sd = h->sd, ad = h->ad;
   int k = 0;
@@ -734,6 +1199,36 @@ static int input_from_ring(td3_handle* h, Ring* r, Plan* P, bool inject_idx, hip
   a.seg[k++] = GatherSeg{P->X_SP, P->ld_sa, 0, r->o_s, sd};
   a.seg[k++] = GatherSeg{P->X_S2, P->ld_s, 0, r->o_s2, sd};
   a.seg[k++] = GatherSeg{P->X_S2A, P->ld_sa, 0, r->o_s2, sd};
+  a.seg[k++] = GatherSeg{P->R, 1, 0, r->o_r, 1};
+  a.seg[k++] = GatherSeg{P->ND, 1, 0, r->o_nd, 1};
+  a.nseg = k;
+  a.B = P->B;
+  a.Bp = P->Bp;
+  a.data = r->data;
+  a.rec = r->rec;
+  a.d_size = r->d_size;
+  a.inject_idx = inject_idx ? P->d_inject_idx : nullptr;
+  a.idx_out = P->d_idx;
+  a.seed = r->seed;
+  a.ctr = h->d_ctr;
+  return launch_gather(a, s);
+}
+
+// Particle rings: the small fields go to every network's MLP input rows; the particle blocks
+// stay in the ring and are read there by the encoders (rows P->d_idx).
+static int input_from_ring_particles(td3_handle* h, Ring* r, Plan* P, bool inject_idx, hipStream_t s) {
+  GatherArgs a{};
+  const int F = h->sd, ad = h->ad, c0 = kEncC2;
+  const bool cdq = h->cdq != 0;
+  int k = 0;
+  a.seg[k++] = GatherSeg{P->XA, P->ld_a, c0, r->o_s, F};
+  a.seg[k++] = GatherSeg{P->XAQ, P->ld_q, c0, r->o_s, F};
+  a.seg[k++] = GatherSeg{P->XTA, P->ld_a, c0, r->o_s2, F};
+  for (int j = 0; j < (cdq ? 2 : 1); ++j) {
+    a.seg[k++] = GatherSeg{P->XQ[j], P->ld_q, c0, r->o_s, F};
+    a.seg[k++] = GatherSeg{P->XQ[j], P->ld_q, c0 + F, r->o_a, ad};
+    a.seg[k++] = GatherSeg{P->XTQ[j], P->ld_q, c0, r->o_s2, F};
+  }
   a.seg[k++] = GatherSeg{P->R, 1, 0, r->o_r, 1};
   a.seg[k++] = GatherSeg{P->ND, 1, 0, r->o_nd, 1};
   a.nseg = k;
@@ -820,10 +1315,22 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
   return 0;
 }
 
+static int build_step_particles(td3_handle* h, int B);
+
+static int build_plan(td3_handle* h, int B) {
+  return h->particles ? build_step_particles(h, B) : build_step(h, B);
+}
+
 static int ensure_plan(td3_handle* h, int B) {
   if (h->plan && h->plan->B == B) return 0;
   TD3_HIP(hipStreamSynchronize(h->stream));
-  return build_step(h, B);
+  return build_plan(h, B);
+}
+
+// A particle learner's encoders read the ring the step samples from.
+static void bind_ring(td3_handle* h, Ring* r) {
+  Plan* P = h->plan.get();
+  if (P->particles) set_particle_source(P, r, r->data, r->rec, r->o_p, r->o_p2, P->d_idx);
 }
 
 static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_stats* stats) {
@@ -833,7 +1340,8 @@ static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_s
   if (!stats) return 0;
   Plan* P = h->plan.get();
   TD3_HIP(hipStreamSynchronize(s));
-  const int B = P->B, Bp = P->Bp;
+  const int B = P->B, Bp = P->Bp, nq = P->nq, ldq = P->ldq;
+  const bool twin = !P->particles || h->cdq;
   std::vector<float> sq(2 * (size_t)Bp);
   TD3_HIP(hipMemcpy(sq.data(), P->sqerr, sq.size() * 4, hipMemcpyDeviceToHost));
   double l1 = 0, l2 = 0;
@@ -841,19 +1349,24 @@ static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_s
     l1 += sq[i];
     l2 += sq[Bp + i];
   }
-  stats->critic_loss = l1 / B + l2 / B;
+  const double n = (double)B * nq;                // F.mse_loss mean over all elements
+  stats->critic_loss = l1 / n + (twin ? l2 / n : 0.0);
   stats->actor_step = actor_phase;
   stats->actor_loss = NAN;
+  auto rows = [&](float* dst, const float* src) -> int {     // [Bp][ldq] -> [B][nq]
+    TD3_HIP(hipMemcpy2D(dst, (size_t)nq * 4, src, (size_t)ldq * 4, (size_t)nq * 4, B, hipMemcpyDeviceToHost));
+    return 0;
+  };
   if (actor_phase) {
-    std::vector<float> q(Bp);
-    TD3_HIP(hipMemcpy(q.data(), P->AQ.Qv, Bp * 4, hipMemcpyDeviceToHost));
+    std::vector<float> q((size_t)B * nq);
+    TD3_RC(rows(q.data(), P->AQ.Qv));
     double m = 0;
-    for (int i = 0; i < B; ++i) m += q[i];
-    stats->actor_loss = -m / B;
+    for (float v : q) m += v;
+    stats->actor_loss = -m / n;
   }
-  if (stats->y) TD3_HIP(hipMemcpy(stats->y, P->Y, B * 4, hipMemcpyDeviceToHost));
-  if (stats->q1) TD3_HIP(hipMemcpy(stats->q1, P->Q[0].Qv, B * 4, hipMemcpyDeviceToHost));
-  if (stats->q2) TD3_HIP(hipMemcpy(stats->q2, P->Q[1].Qv, B * 4, hipMemcpyDeviceToHost));
+  if (stats->y) TD3_RC(rows(stats->y, P->Y));
+  if (stats->q1) TD3_RC(rows(stats->q1, P->Q[0].Qv));
+  if (stats->q2) TD3_RC(rows(stats->q2, P->Q[twin ? 1 : 0].Qv));
   if (stats->idx) TD3_HIP(hipMemcpy(stats->idx, P->d_idx, B * 8, hipMemcpyDeviceToHost));
   if (stats->noise) TD3_HIP(hipMemcpy(stats->noise, P->noise, (size_t)B * h->ad * 4, hipMemcpyDeviceToHost));
   return 0;
@@ -923,6 +1436,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     for (int j = 0; j < 2; ++j) {
       HeadProb p = head(j ? q2 : q1, h->critic.P, A->Q[j], kHeadQ);
       p.out = A->Q[j].Qv;
+      p.ldo = 1;
       hp.push_back(p);
     }
     void* d = nullptr;
@@ -934,6 +1448,119 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     a.max_action = h->cfg.max_action;
     A->evalq.push_back({"evq_head", [=](hipStream_t s) { return launch_heads(a, 2, s); }, 0});
   }
+  *out = A.get();
+  h->act[Bp] = std::move(A);
+  return 0;
+}
+
+// select_action / eval_q of TD3_particles (TD3_particles.py:153-164): the particles of the n
+// query states are uploaded packed ([n][N*D], rows 0..n-1), the encoders read them in place.
+static int build_act_particles(td3_handle* h, int Bp, ActPlan** out) {
+  auto it = h->act.find(Bp);
+  if (it != h->act.end()) {
+    *out = it->second.get();
+    return 0;
+  }
+  std::unique_ptr<ActPlan> A(new ActPlan());
+  A->Bp = Bp;
+  const bool norm = h->cfg.norm != 0;
+  const bool cdq = h->cdq != 0;
+  const int N = h->N, D = h->D, ad = h->ad;
+  const NetL& an = h->actor.nets[0];
+  const NetL& q1 = h->critic.nets[0];
+  const NetL& q2 = h->critic.nets[cdq ? 1 : 0];
+  const int lda = an.lin[0].Kp, ldq = q1.lin[0].Kp;
+  size_t floats = (size_t)Bp * (lda + 2 * ldq) + (size_t)Bp * N * D + (size_t)Bp * 32 + 2 * (size_t)Bp +
+                  eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, false, norm) + 8192;
+  TD3_HIP(hipMalloc(&A->scratch, floats * 4));
+  TD3_HIP(hipMemset(A->scratch, 0, floats * 4));
+  Scratch S{A->scratch, floats, 0};
+  A->X_S = S.take((size_t)Bp * lda);
+  A->X_SA = S.take((size_t)Bp * ldq);
+  A->XQ2 = S.take((size_t)Bp * ldq);
+  A->pbatch = S.take((size_t)Bp * N * D);
+  A->out = S.take((size_t)Bp * 32);
+  A->d_iota = (int64_t*)S.take(2 * (size_t)Bp);
+  alloc_eval(S, an, Bp, A->X_S, lda, false, norm, true, A->A);
+  alloc_eval(S, q1, Bp, A->X_SA, ldq, false, norm, true, A->Q[0]);
+  alloc_eval(S, q2, Bp, A->XQ2, ldq, false, norm, true, A->Q[1]);
+  {
+    std::vector<int64_t> iota(Bp);
+    for (int i = 0; i < Bp; ++i) iota[i] = i;
+    TD3_HIP(hipMemcpy(A->d_iota, iota.data(), Bp * 8, hipMemcpyHostToDevice));
+  }
+  auto enc_stage = [&](std::vector<Stage>& st, std::vector<EncFwdProb> probs, const char* name) {
+    EncFwdArgs a{};
+    for (size_t k = 0; k < probs.size(); ++k) a.p[k] = probs[k];
+    a.nprob = (int)probs.size();
+    a.data = A->pbatch;
+    a.rec = N * D;
+    a.idx = A->d_iota;
+    a.B = Bp;
+    a.Bp = Bp;
+    a.N = N;
+    a.D = D;
+    a.ntile = (N + 31) / 32;
+    st.push_back({name, [=](hipStream_t s) { return launch_enc_fwd(a, s); }, 0, "td3::enc_fwd_kernel"});
+  };
+  auto head = [&](const NetL& n, const float* Pp, EvalB& e, int mode) {
+    HeadProb q{};
+    q.H3 = e.H[2];
+    q.ldh = n.lin[2].Np;
+    q.K3 = n.lin[2].N;
+    q.lng = norm ? Pp + n.ln[2].offg : nullptr;
+    q.lnb = norm ? Pp + n.ln[2].offb : nullptr;
+    q.W4 = Pp + n.lin[3].offW;
+    q.ldw = n.lin[3].Kp;
+    q.b4 = Pp + n.lin[3].offb;
+    q.nout = n.lin[3].N;
+    q.mode = mode;
+    return q;
+  };
+  const float* Pa = h->actor.P;
+  const float* Pq = h->critic.P;
+  {
+    enc_stage(A->act, {EncFwdProb{Pa + an.enc_off, 0, A->X_S, lda, nullptr}}, "act_enc");
+    std::vector<FwdItem> f = {{&an, Pa, &A->A, false, false}};
+    TD3_RC(add_fwd_stages(h, A->tables, A->act, f, Bp, Bp, "act", nullptr, 0));
+    HeadProb p = head(an, Pa, A->A, kHeadPolicy);
+    p.out = A->out;
+    p.ldo = 32;
+    p.out_col = 0;
+    void* d = nullptr;
+    TD3_RC(upload(h, A->tables, &p, sizeof(p), &d));
+    HeadArgs a{};
+    a.probs = (const HeadProb*)d;
+    a.B = Bp;
+    a.Bp = Bp;
+    a.max_action = 1.0f;                              // tanh policy (TD3_particles.py:68)
+    A->act.push_back({"act_head", [=](hipStream_t s) { return launch_heads(a, 1, s); }, 0});
+  }
+  {
+    std::vector<EncFwdProb> ep = {EncFwdProb{Pq + q1.enc_off, 0, A->X_SA, ldq, nullptr}};
+    if (cdq) ep.push_back(EncFwdProb{Pq + q2.enc_off, 0, A->XQ2, ldq, nullptr});
+    enc_stage(A->evalq, ep, "evq_enc");
+    std::vector<FwdItem> f = {{&q1, Pq, &A->Q[0], false, false}};
+    if (cdq) f.push_back({&q2, Pq, &A->Q[1], false, false});
+    TD3_RC(add_fwd_stages(h, A->tables, A->evalq, f, Bp, Bp, "evq", nullptr, 0));
+    std::vector<HeadProb> hp;
+    for (int j = 0; j < (cdq ? 2 : 1); ++j) {
+      HeadProb p = head(j ? q2 : q1, Pq, A->Q[j], kHeadQ);
+      p.out = A->Q[j].Qv;
+      p.ldo = 32;
+      hp.push_back(p);
+    }
+    void* d = nullptr;
+    TD3_RC(upload(h, A->tables, hp.data(), hp.size() * sizeof(HeadProb), &d));
+    HeadArgs a{};
+    a.probs = (const HeadProb*)d;
+    a.B = Bp;
+    a.Bp = Bp;
+    a.max_action = 1.0f;
+    const int nh = (int)hp.size();
+    A->evalq.push_back({"evq_head", [=](hipStream_t s) { return launch_heads(a, nh, s); }, 0});
+  }
+  (void)ad;
   *out = A.get();
   h->act[Bp] = std::move(A);
   return 0;
@@ -970,6 +1597,8 @@ void td3_default_config(td3_config* c) {
   c->seed = 0;
   c->device = 0;
   c->use_graph = 1;
+  c->particles = 0;
+  c->cdq = 1;
 }
 
 int td3_create(const td3_config* cfg, td3_handle** out) {
@@ -977,25 +1606,48 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_ARG(cfg->state_dim > 0 && cfg->action_dim > 0, "dims must be positive");
   TD3_ARG(cfg->action_dim <= 32, "action_dim > 32 not supported by the head kernels");
   TD3_ARG(cfg->policy_freq > 0, "policy_freq must be positive");
-  TD3_ARG(pad32(cfg->state_dim + cfg->action_dim) <= 512, "state_dim + action_dim must be <= 512");
+  const int in_extra = cfg->particles ? kEncC2 : 0;
+  TD3_ARG(pad32(in_extra + cfg->state_dim + cfg->action_dim) <= 512, "network input width must be <= 512");
+  if (cfg->particles) {
+    TD3_ARG(cfg->n_particles > 0 && cfg->particle_dim > 0, "particle shape must be positive");
+    TD3_ARG(cfg->particle_dim <= kEncMaxD, "particle_dim > 16 not supported by the encoder kernels");
+  }
   for (int i = 0; i < 3; ++i) {
     TD3_ARG(cfg->actor_hidden[i] > 0 && cfg->actor_hidden[i] <= 512, "actor hidden in (0, 512]");
     TD3_ARG(cfg->critic_hidden[i] > 0 && cfg->critic_hidden[i] <= 512, "critic hidden in (0, 512]");
   }
   TD3_HIP(hipSetDevice(cfg->device));
   TD3_RC(kernels_init());
+  TD3_RC(encoder_init());
   td3_handle* h = new td3_handle();
   h->cfg = *cfg;
   h->sd = cfg->state_dim;
   h->ad = cfg->action_dim;
   const bool norm = cfg->norm != 0;
   int64_t off = 0;
-  h->actor.nets.push_back(layout_mlp(h->sd, cfg->actor_hidden, h->ad, norm, "", off, h->actor.tensors));
-  h->actor.size = off;
-  off = 0;
-  h->critic.nets.push_back(layout_mlp(h->sd + h->ad, cfg->critic_hidden, 1, norm, "q1.", off, h->critic.tensors));
-  h->critic.nets.push_back(layout_mlp(h->sd + h->ad, cfg->critic_hidden, 1, norm, "q2.", off, h->critic.tensors));
-  h->critic.size = off;
+  if (cfg->particles) {                     // TD3_particles.py:19-50 (Actor), :71-128 (Critic)
+    h->particles = 1;
+    h->N = cfg->n_particles;
+    h->D = cfg->particle_dim;
+    h->cdq = cfg->cdq ? 1 : 0;
+    const int F = h->sd, A = h->ad, D = h->D;
+    h->actor.nets.push_back(layout_mlp(kEncC2 + F, cfg->actor_hidden, A, norm, "", off, h->actor.tensors, D));
+    h->actor.size = (off + 63) & ~(int64_t)63;
+    off = 0;
+    h->critic.nets.push_back(
+        layout_mlp(kEncC2 + F + A, cfg->critic_hidden, A, norm, "q1.", off, h->critic.tensors, D));
+    if (h->cdq)
+      h->critic.nets.push_back(
+          layout_mlp(kEncC2 + F + A, cfg->critic_hidden, A, norm, "q2.", off, h->critic.tensors, D));
+    h->critic.size = (off + 63) & ~(int64_t)63;
+  } else {
+    h->actor.nets.push_back(layout_mlp(h->sd, cfg->actor_hidden, h->ad, norm, "", off, h->actor.tensors));
+    h->actor.size = off;
+    off = 0;
+    h->critic.nets.push_back(layout_mlp(h->sd + h->ad, cfg->critic_hidden, 1, norm, "q1.", off, h->critic.tensors));
+    h->critic.nets.push_back(layout_mlp(h->sd + h->ad, cfg->critic_hidden, 1, norm, "q2.", off, h->critic.tensors));
+    h->critic.size = off;
+  }
   const size_t total = 5 * (size_t)(h->actor.size + h->critic.size);
   hipError_t e = hipMalloc(&h->arena, total * sizeof(float));
   if (e != hipSuccess) {
@@ -1156,8 +1808,11 @@ int td3_train_step(td3_handle* h, rb_handle* rbh, int batch, void* stream, const
   TD3_ARG(r->size > 0 || inject_idx, "train on an empty replay buffer");
   TD3_ARG(r->device == h->cfg.device, "replay buffer lives on another device");
   TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_ARG(r->particles == h->particles, "replay buffer kind does not match the learner");
+  TD3_ARG(!r->particles || (r->N == h->N && r->D == h->D), "particle shape does not match the learner");
   TD3_RC(ensure_plan(h, batch));
   Plan* P = h->plan.get();
+  bind_ring(h, r);
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
   TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
   if (inject_idx) {
@@ -1184,6 +1839,7 @@ int td3_train_step_batch(td3_handle* h, const float* state, const float* action,
   TD3_ARG(h != nullptr, "null handle");
   TD3_ARG(state && action && next_state && reward && not_done, "null input");
   TD3_ARG(batch > 0, "batch must be positive");
+  TD3_ARG(!h->particles, "td3_train_step_batch on a particle learner (use td3_train_step_batch_particles)");
   TD3_HIP(hipSetDevice(h->cfg.device));
   TD3_RC(ensure_plan(h, batch));
   Plan* P = h->plan.get();
@@ -1199,6 +1855,7 @@ int td3_train_step_batch(td3_handle* h, const float* state, const float* action,
 
 int td3_select_action(td3_handle* h, const float* state, float* action_out, int n) {
   TD3_ARG(h && state && action_out, "null argument");
+  TD3_ARG(!h->particles, "particle learner: use td3_select_action_particles");
   TD3_ARG(n > 0, "n must be positive");
   TD3_HIP(hipSetDevice(h->cfg.device));
   ActPlan* A;
@@ -1214,6 +1871,7 @@ int td3_select_action(td3_handle* h, const float* state, float* action_out, int 
 
 int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_out, int n) {
   TD3_ARG(h && state && action && q_out, "null argument");
+  TD3_ARG(!h->particles, "particle learner: use td3_eval_q_particles");
   TD3_ARG(n > 0, "n must be positive");
   TD3_HIP(hipSetDevice(h->cfg.device));
   ActPlan* A;
@@ -1225,6 +1883,93 @@ int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_
   TD3_RC(run_stages(A->evalq, s));
   TD3_HIP(hipMemcpyAsync(q_out, A->Q[0].Qv, (size_t)n * 4, hipMemcpyDeviceToHost, s));
   TD3_HIP(hipMemcpyAsync(q_out + n, A->Q[1].Qv, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  TD3_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int td3_train_step_batch_particles(td3_handle* h, const float* feat, const float* part, const float* action,
+                                   const float* next_feat, const float* next_part, const float* reward,
+                                   const float* not_done, int batch, void* stream, const float* inject_noise,
+                                   td3_step_stats* stats) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(h->particles, "td3_train_step_batch_particles on a featured learner");
+  TD3_ARG(feat && part && action && next_feat && next_part && reward && not_done, "null input");
+  TD3_ARG(batch > 0, "batch must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_RC(ensure_plan(h, batch));
+  Plan* P = h->plan.get();
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  const int F = h->sd, ad = h->ad, B = P->B, Bp = P->Bp, np = h->N * h->D, c0 = kEncC2;
+  const bool cdq = h->cdq != 0;
+  set_particle_source(P, P->pbatch, P->pbatch, 2 * np, 0, np, P->d_iota);
+  if (inject_noise)
+    TD3_HIP(hipMemcpyAsync(P->noise, inject_noise, (size_t)batch * ad * 4, hipMemcpyHostToDevice, s));
+  // the sampled tensors -> MLP input rows and the packed particle rows (s | s')
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, feat, F, B, Bp, P->XA, P->ld_a, c0, P->XAQ, P->ld_q,
+                     c0, P->XQ[0], P->ld_q, c0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, action, ad, B, Bp, P->XQ[0], P->ld_q, c0 + F,
+                     cdq ? P->XQ[1] : (float*)nullptr, P->ld_q, c0 + F, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, next_feat, F, B, Bp, P->XTA, P->ld_a, c0,
+                     P->XTQ[0], P->ld_q, c0, cdq ? P->XTQ[1] : (float*)nullptr, P->ld_q, c0);
+  if (cdq)
+    hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, feat, F, B, Bp, P->XQ[1], P->ld_q, c0,
+                       (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, part, np, B, Bp, P->pbatch, 2 * np, 0,
+                     (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, next_part, np, B, Bp, P->pbatch, 2 * np, np,
+                     (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, reward, 1, B, Bp, P->R, 1, 0, (float*)nullptr, 0, 0,
+                     (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, not_done, 1, B, Bp, P->ND, 1, 0, (float*)nullptr, 0,
+                     0, (float*)nullptr, 0, 0);
+  TD3_HIP(hipGetLastError());
+  const int actor_phase = ((h->total_it + 1) % h->cfg.policy_freq) == 0;
+  TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s, nullptr));
+  if (inject_noise) TD3_HIP(hipStreamSynchronize(s));
+  return finish_step(h, actor_phase, s, stats);
+}
+
+int td3_select_action_particles(td3_handle* h, const float* feat, const float* part, float* action_out, int n) {
+  TD3_ARG(h && feat && part && action_out, "null argument");
+  TD3_ARG(h->particles, "not a particle learner");
+  TD3_ARG(n > 0, "n must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  ActPlan* A;
+  TD3_RC(build_act_particles(h, pad32(n), &A));
+  hipStream_t s = h->stream;
+  const int np = h->N * h->D;
+  const NetL& an = h->actor.nets[0];
+  TD3_RC(copy_rows_h2d(A->X_S, an.lin[0].Kp, kEncC2, feat, n, h->sd, s));
+  TD3_HIP(hipMemcpyAsync(A->pbatch, part, (size_t)n * np * 4, hipMemcpyHostToDevice, s));
+  TD3_RC(run_stages(A->act, s));
+  TD3_HIP(hipMemcpy2DAsync(action_out, (size_t)h->ad * 4, A->out, 32 * 4, (size_t)h->ad * 4, n,
+                           hipMemcpyDeviceToHost, s));
+  TD3_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int td3_eval_q_particles(td3_handle* h, const float* feat, const float* part, const float* action, float* q_out,
+                         int n) {
+  TD3_ARG(h && feat && part && action && q_out, "null argument");
+  TD3_ARG(h->particles, "not a particle learner");
+  TD3_ARG(n > 0, "n must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  ActPlan* A;
+  TD3_RC(build_act_particles(h, pad32(n), &A));
+  hipStream_t s = h->stream;
+  const int np = h->N * h->D, F = h->sd, ad = h->ad;
+  const int ldq = h->critic.nets[0].lin[0].Kp;
+  const bool cdq = h->cdq != 0;
+  for (float* X : {A->X_SA, A->XQ2}) {
+    if (X == A->XQ2 && !cdq) continue;
+    TD3_RC(copy_rows_h2d(X, ldq, kEncC2, feat, n, F, s));
+    TD3_RC(copy_rows_h2d(X, ldq, kEncC2 + F, action, n, ad, s));
+  }
+  TD3_HIP(hipMemcpyAsync(A->pbatch, part, (size_t)n * np * 4, hipMemcpyHostToDevice, s));
+  TD3_RC(run_stages(A->evalq, s));
+  for (int j = 0; j < 2; ++j)
+    TD3_HIP(hipMemcpy2DAsync(q_out + (size_t)j * n * ad, (size_t)ad * 4, A->Q[cdq ? j : 0].Qv, 32 * 4,
+                             (size_t)ad * 4, n, hipMemcpyDeviceToHost, s));
   TD3_HIP(hipStreamSynchronize(s));
   return 0;
 }
@@ -1260,7 +2005,7 @@ int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int ra
   h->rank = rank;
   if (h->plan) {           // stage lists change (grad write + all-reduce + flat Adam)
     int B = h->plan->B;
-    TD3_RC(build_step(h, B));
+    TD3_RC(build_plan(h, B));
   }
   return 0;
 }
@@ -1281,6 +2026,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   TD3_HIP(hipSetDevice(h->cfg.device));
   TD3_RC(ensure_plan(h, batch));
   Plan* P = h->plan.get();
+  bind_ring(h, r);
   std::vector<Stage>& st = P->body[actor_phase ? 1 : 0][0];
   const int n = (int)st.size() + 1;
   TD3_ARG(max_stages >= n, "max_stages too small");

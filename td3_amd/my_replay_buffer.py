@@ -5,6 +5,7 @@ Drop-in for ``/root/reference/my_replay_buffer.py``:
 * ``ReplayBuffer_featured(obs_space, action_space, max_size=1e6, load_folder=None)``
   (:72-89) with ``add`` (:109-117), ``sample`` (:119-128), ``save`` / ``load``
   (:91-107) and the ``ptr`` / ``size`` / ``max_size`` attributes.
+* ``ReplayBuffer_particles`` (:6-69), the same over (features, particles) states.
 
 The storage lives in HBM (``libtd3hip``'s ring, one fp32 record per transition).
 ``add`` stages rows on the host and ships them in batches (pinned memory, async
@@ -232,6 +233,202 @@ class ReplayBuffer_featured(object):
         rec[:, sd + ad:2 * sd + ad] = arrs["next_state"]
         rec[:, 2 * sd + ad] = arrs["reward"].reshape(n)
         rec[:, 2 * sd + ad + 1] = arrs["not_done"].reshape(n)
+        check(self._lib.rb_write_records(self._h, 0, n, _lib.fptr(rec), ptr % n, min(size, n)),
+              "rb_write_records")
+
+    def __del__(self):
+        try:
+            if self._h is not None and _lib.alive():
+                self._lib.rb_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class ReplayBuffer_particles(object):
+    """Particle-observation replay ring (my_replay_buffer.py:6-69) resident in HBM.
+
+    ``obs_space`` is the reference's 2-tuple of Boxes: features ``[F]`` and particles
+    ``[N, D]`` (TD3_particles.py:29, :37); a state is the tuple ``(features, particles)``.
+    One fp32 record per transition holds both states; the learner's encoders read the
+    particle blocks in place, so ``TD3.train`` moves no particle bytes for sampling.
+    """
+
+    store_np = ["state_features", "state_particles", "action", "next_state_features",
+                "next_state_particles", "reward", "not_done"]
+    store_pkl = ["ptr", "size"]
+
+    def __init__(self, obs_space, action_space, max_size=int(1e6), load_folder=None,
+                 device=None, seed=0):
+        self._lib = _lib.load()
+        self.feat_dim = int(obs_space[0].shape[0])
+        self.n_particles, self.particle_dim = (int(x) for x in obs_space[1].shape)
+        self.action_dim = int(action_space.shape[0])
+        self._dev = default_device_index() if device is None else int(device)
+        torch = _torch()
+        self.device = torch.device("cuda", self._dev)
+        self.seed = int(seed)
+        self._h = None
+        self._pending = []
+        if load_folder is not None:
+            self.load(load_folder)
+        else:
+            self._create(int(max_size))
+
+    def _create(self, max_size):
+        import ctypes as C
+        if self._h is not None:
+            self._lib.rb_destroy(self._h)
+            self._h = None
+        h = C.c_void_p()
+        check(self._lib.rb_create_particles(self.feat_dim, self.n_particles, self.particle_dim,
+                                            self.action_dim, max_size, self._dev, self.seed,
+                                            C.byref(h)), "rb_create_particles")
+        self._h = h
+        self.max_size = max_size
+        self.record_floats = self._info().record_floats
+
+    def _info(self):
+        info = _lib.rb_info_t()
+        check(self._lib.rb_info(self._h, info), "rb_info")
+        return info
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def ptr(self):
+        self.flush()
+        return int(self._info().ptr)
+
+    @property
+    def size(self):
+        self.flush()
+        return int(self._info().size)
+
+    def _stream(self):
+        return _torch().cuda.current_stream(self.device).cuda_stream
+
+    def _np(self):
+        return self.n_particles * self.particle_dim
+
+    # ------------------------------------------------------------------ reference API
+    def add(self, state, action, next_state, reward, done):
+        """my_replay_buffer.py:46-56 (state = (features, particles); stores 1 - done)."""
+        F, npd = self.feat_dim, self._np()
+        self._pending.append((np.asarray(state[0], dtype=np.float64).reshape(F),
+                              np.asarray(state[1], dtype=np.float64).reshape(npd),
+                              np.asarray(action, dtype=np.float64).reshape(self.action_dim),
+                              np.asarray(next_state[0], dtype=np.float64).reshape(F),
+                              np.asarray(next_state[1], dtype=np.float64).reshape(npd),
+                              float(np.asarray(reward, dtype=np.float64).reshape(-1)[0]),
+                              float(np.asarray(done, dtype=np.float64).reshape(-1)[0])))
+        if len(self._pending) >= max(1, _STAGE_ROWS // 16):
+            self.flush()
+
+    def add_batch(self, feat, part, action, next_feat, next_part, reward, done):
+        self.flush()
+        F, npd, A = self.feat_dim, self._np(), self.action_dim
+        f = np.ascontiguousarray(feat, dtype=np.float64).reshape(-1, F)
+        n = f.shape[0]
+        arrs = [f, np.ascontiguousarray(part, dtype=np.float64).reshape(n, npd),
+                np.ascontiguousarray(action, dtype=np.float64).reshape(n, A),
+                np.ascontiguousarray(next_feat, dtype=np.float64).reshape(n, F),
+                np.ascontiguousarray(next_part, dtype=np.float64).reshape(n, npd),
+                np.ascontiguousarray(reward, dtype=np.float64).reshape(n),
+                np.ascontiguousarray(done, dtype=np.float64).reshape(n)]
+        check(self._lib.rb_add_particles(self._h, *[_lib.dptr(x) for x in arrs], n, self._stream()),
+              "rb_add_particles")
+
+    def flush(self):
+        if not self._pending:
+            return
+        rows = self._pending
+        self._pending = []
+        cols = [np.stack([r[i] for r in rows]) for i in range(5)]
+        cols += [np.array([r[5] for r in rows], dtype=np.float64), np.array([r[6] for r in rows], dtype=np.float64)]
+        check(self._lib.rb_add_particles(self._h, *[_lib.dptr(np.ascontiguousarray(x)) for x in cols],
+                                         len(rows), self._stream()), "rb_add_particles")
+
+    def fill_synthetic(self, n, max_action=1.0, seed=0):
+        self.flush()
+        check(self._lib.rb_fill_synthetic(self._h, int(n), float(max_action), int(seed), self._stream()),
+              "rb_fill_synthetic")
+
+    def sample(self, batch_size, indices=None, return_indices=False):
+        """my_replay_buffer.py:58-69: the 7 fp32 device tensors."""
+        torch = _torch()
+        self.flush()
+        B = int(batch_size)
+        dev = self.device
+        N, D, F, A = self.n_particles, self.particle_dim, self.feat_dim, self.action_dim
+        out = (torch.empty((B, F), device=dev), torch.empty((B, N, D), device=dev),
+               torch.empty((B, A), device=dev), torch.empty((B, F), device=dev),
+               torch.empty((B, N, D), device=dev), torch.empty((B, 1), device=dev),
+               torch.empty((B, 1), device=dev))
+        idx_out = torch.empty((B,), device=dev, dtype=torch.int64)
+        inj = None
+        if indices is not None:
+            inj = torch.as_tensor(np.asarray(indices, dtype=np.int64), device=dev)
+            if inj.numel() != B:
+                raise ValueError("indices must have batch_size entries")
+            size = self.size
+            if B and (int(inj.min()) < 0 or int(inj.max()) >= max(size, 1)):
+                raise IndexError("index out of range of the filled buffer")
+        check(self._lib.rb_sample_particles(self._h, B, *[t.data_ptr() for t in out],
+                                            inj.data_ptr() if inj is not None else None,
+                                            idx_out.data_ptr(), self._stream()), "rb_sample_particles")
+        if return_indices:
+            return out, idx_out
+        return out
+
+    # ------------------------------------------------------------------ persistence
+    def _offsets(self):
+        F, npd, A = self.feat_dim, self._np(), self.action_dim
+        o = {}
+        c = 0
+        for name, w in (("state_features", F), ("state_particles", npd), ("action", A),
+                        ("next_state_features", F), ("next_state_particles", npd), ("reward", 1),
+                        ("not_done", 1)):
+            o[name] = (c, w)
+            c += w
+        return o
+
+    def save(self, folder):
+        """my_replay_buffer.py:24-32 (ptr / size pickled with protocol 4, arrays np.save'd)."""
+        self.flush()
+        os.makedirs(folder, exist_ok=True)
+        info = self._info()
+        for attrib, v in (("ptr", int(info.ptr)), ("size", int(info.size))):
+            with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
+                pickle.dump(v, f, protocol=4)
+        n = self.max_size
+        rec = np.empty((n, self.record_floats), dtype=np.float32)
+        check(self._lib.rb_read_records(self._h, 0, n, _lib.fptr(rec)), "rb_read_records")
+        shapes = {"state_particles": (n, self.n_particles, self.particle_dim),
+                  "next_state_particles": (n, self.n_particles, self.particle_dim)}
+        for name, (c, w) in self._offsets().items():
+            arr = rec[:, c:c + w].astype(np.float64).reshape(shapes.get(name, (n, w)))
+            with open(os.path.join(folder, name + ".pkl"), "wb") as f:
+                np.save(f, arr)
+
+    def load(self, folder):
+        """my_replay_buffer.py:34-44 (int-only unpickler for ptr / size)."""
+        ptr = _load_int(os.path.join(folder, "ptr.pkl"))
+        size = _load_int(os.path.join(folder, "size.pkl"))
+        arrs = {}
+        for attrib in self.store_np:
+            with open(os.path.join(folder, attrib + ".pkl"), "rb") as f:
+                arrs[attrib] = np.load(f, allow_pickle=False)
+        n = arrs["state_features"].shape[0]
+        self.feat_dim = arrs["state_features"].shape[1]
+        self.n_particles, self.particle_dim = arrs["state_particles"].shape[1:3]
+        self.action_dim = arrs["action"].shape[1]
+        self._create(n)
+        rec = np.zeros((n, self.record_floats), dtype=np.float32)
+        for name, (c, w) in self._offsets().items():
+            rec[:, c:c + w] = arrs[name].reshape(n, w)
         check(self._lib.rb_write_records(self._h, 0, n, _lib.fptr(rec), ptr % n, min(size, n)),
               "rb_write_records")
 
