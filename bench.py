@@ -30,7 +30,24 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-SD, AD, MAX_ACTION, BATCH, REPLAY = 17, 6, 1.0, 256, 1_000_000
+
+# BASELINE.json configs besides the headline one (``--config``): C3 Humanoid-v4 TD3_featured
+# B=1024 replay 2e6, C4 water-pouring particles TD3_particles B=4096 (F=7, N=350, D=9, A=3 as
+# assumed in SURVEY.md §8d) replay 1e5.
+CONFIGS = {
+    "halfcheetah": dict(kind="featured", sd=17, ad=6, ma=1.0, batch=256, replay=1_000_000,
+                        workload="TD3_featured.train(replay_buffer, 256) on HalfCheetah-v4 shapes "
+                                 "(state 17, action 6, actor 500-400-300, critic 2x 500-400-200, "
+                                 "LayerNorm, policy_freq 2), replay 1e6 per GPU"),
+    "humanoid": dict(kind="featured", sd=376, ad=17, ma=0.4, batch=1024, replay=2_000_000,
+                     workload="TD3_featured.train(replay_buffer, 1024) on Humanoid-v4 shapes "
+                              "(state 376, action 17, actor 500-400-300, critic 2x 500-400-200, "
+                              "LayerNorm, policy_freq 2), replay 2e6 per GPU"),
+    "particles": dict(kind="particles", F=7, N=350, D=9, ad=3, ma=1.0, batch=4096, replay=100_000,
+                      workload="TD3_particles.train(replay_buffer, 4096): features 7, 350 particles x 9, "
+                               "action 3, encoders conv1 256 / conv2 128, MLP 500-400-300 with lnorm1 + "
+                               "LayerNorm, CDQ, policy_freq 2, replay 1e5 per GPU"),
+}
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8 TB/s spec
 FP32_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: f32 MFMA / vector peak
 
@@ -40,14 +57,14 @@ class Box:
         self.shape = tuple(shape)
 
 
-def stage_table(pol, rb, iters=50):
+def stage_table(pol, rb, batch, iters=50):
     """Per-stage mean device time (HIP events, handle stream) for an odd and an even step."""
     lib, h = pol._lib, pol._h
     rows = []
     ms = (C.c_float * 128)()
     n = C.c_int()
     for phase in (0, 1):
-        rc = lib.td3_profile_stages(h, rb.handle, BATCH, phase, ms, 128, C.byref(n))
+        rc = lib.td3_profile_stages(h, rb.handle, batch, phase, ms, 128, C.byref(n))
         if rc:
             raise RuntimeError(lib.td3_last_error().decode())
         names = [lib.td3_stage_name(h, i).decode() for i in range(n.value)]
@@ -88,9 +105,9 @@ def roofline_from_stages(rows, pmc):
             "flops_per_launch": per_launch_flops}, fam
 
 
-def cpu_baseline(seconds=12.0):
-    """The numpy oracle (oracle/td3_oracle.py, a restatement of TD3_featured.train pinned to
-    the reference's goldens) on this host's cores: same shapes, B=256."""
+def cpu_baseline(cfg, seconds=12.0):
+    """The numpy oracle (oracle/td3_oracle.py, a restatement of TD3_*.train pinned to the
+    reference's goldens) on this host's cores: same shapes and batch as the GPU line."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import gen
     from oracle import td3_oracle as orc
@@ -99,31 +116,44 @@ def cpu_baseline(seconds=12.0):
         cores = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
     except Exception:
         cores = os.cpu_count() or 1
-    a0 = gen.init_params(gen.featured_actor_shapes(SD, AD, "layer"), 1)
-    c0 = gen.init_params(gen.featured_critic_shapes(SD, AD, "layer"), 2)
-    L = orc.Learner(a0, c0, max_action=MAX_ACTION, norm="layer")
-    rows = 20000
-    buf = orc.FeaturedBuffer(SD, AD, rows)
+    B, ad = cfg["batch"], cfg["ad"]
     rs = np.random.RandomState(0)
-    buf.state[:] = rs.standard_normal((rows, SD))
-    buf.action[:] = rs.uniform(-1, 1, (rows, AD))
-    buf.next_state[:] = rs.standard_normal((rows, SD))
+    rows = 2048 if cfg["kind"] == "particles" else 20000
+    if cfg["kind"] == "particles":
+        F, N, D = cfg["F"], cfg["N"], cfg["D"]
+        a0 = gen.init_params(gen.particle_actor_shapes(F, D, ad, "layer"), 1)
+        c0 = gen.init_params(gen.particle_critic_shapes(F, D, ad, "layer"), 2)
+        L = orc.Learner(a0, c0, norm="layer")
+        buf = orc.ParticleBuffer(F, N, D, ad, rows)
+        buf.state_features[:] = rs.standard_normal(buf.state_features.shape)
+        buf.state_particles[:] = rs.standard_normal(buf.state_particles.shape)
+        buf.next_state_features[:] = rs.standard_normal(buf.next_state_features.shape)
+        buf.next_state_particles[:] = rs.standard_normal(buf.next_state_particles.shape)
+        step, what = orc.particle_train_step, "particles F7 N350 D9 A3"
+    else:
+        sd = cfg["sd"]
+        a0 = gen.init_params(gen.featured_actor_shapes(sd, ad, "layer"), 1)
+        c0 = gen.init_params(gen.featured_critic_shapes(sd, ad, "layer"), 2)
+        L = orc.Learner(a0, c0, max_action=cfg["ma"], norm="layer")
+        buf = orc.FeaturedBuffer(sd, ad, rows)
+        buf.state[:] = rs.standard_normal((rows, sd))
+        buf.next_state[:] = rs.standard_normal((rows, sd))
+        step, what = orc.featured_train_step, f"state {sd} action {ad}"
+    buf.action[:] = rs.uniform(-cfg["ma"], cfg["ma"], buf.action.shape)
     buf.reward[:] = rs.standard_normal((rows, 1))
     buf.not_done[:] = (rs.uniform(size=(rows, 1)) > 0.01)
     buf.size = rows
     steps = 0
-    orc.featured_train_step(L, buf.gather(rs.randint(0, rows, BATCH)),
-                            rs.standard_normal((BATCH, AD)).astype(np.float32))  # warm
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds or steps < 4:
-        idx = rs.randint(0, rows, BATCH)
-        noise = rs.standard_normal((BATCH, AD)).astype(np.float32)
-        orc.featured_train_step(L, buf.gather(idx), noise)
+    while time.perf_counter() - t0 < seconds or steps < 2:
+        idx = rs.randint(0, rows, B)
+        noise = rs.standard_normal((B, ad)).astype(np.float32)
+        step(L, buf.gather(idx), noise)
         steps += 1
     dt = time.perf_counter() - t0
-    return {"value": round(steps / dt, 3), "unit": "grad-steps/s", "cores": int(cores),
+    return {"value": round(steps / dt, 4), "unit": "grad-steps/s", "cores": int(cores),
             "kind": "port",
-            "sample": f"{steps} oracle train steps (HalfCheetah dims, B=256, norm=layer) in {dt:.1f} s"}
+            "sample": f"{steps} oracle train steps ({what}, B={B}, norm=layer) in {dt:.1f} s"}
 
 
 def main():
@@ -131,10 +161,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="halfcheetah")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="disable hipGraph replay")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    B, REPLAY_ROWS = cfg["batch"], cfg["replay"]
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,14 +180,22 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from td3_amd import _lib
-    from td3_amd.TD3_featured import TD3
-    from td3_amd.my_replay_buffer import ReplayBuffer_featured
 
-    torch.manual_seed(1000 + rank if world == 1 else 1000)   # same init on every rank
-    pol = TD3(Box((SD,)), Box((AD,)), max_action=MAX_ACTION, norm="layer", device=local,
-              seed=17 + rank, use_graph=not args.eager)
-    rb = ReplayBuffer_featured(Box((SD,)), Box((AD,)), max_size=REPLAY, device=local, seed=101 + rank)
-    rb.fill_synthetic(REPLAY, MAX_ACTION, seed=7 + rank)
+    torch.manual_seed(1000)                         # same init on every rank
+    if cfg["kind"] == "particles":
+        from td3_amd.TD3_particles import TD3
+        from td3_amd.my_replay_buffer import ReplayBuffer_particles as RB
+        obs = (Box((cfg["F"],)), Box((cfg["N"], cfg["D"])))
+        pol = TD3(obs, Box((cfg["ad"],)), norm="layer", device=local, seed=17 + rank,
+                  use_graph=not args.eager)
+    else:
+        from td3_amd.TD3_featured import TD3
+        from td3_amd.my_replay_buffer import ReplayBuffer_featured as RB
+        obs = Box((cfg["sd"],))
+        pol = TD3(obs, Box((cfg["ad"],)), max_action=cfg["ma"], norm="layer", device=local,
+                  seed=17 + rank, use_graph=not args.eager)
+    rb = RB(obs, Box((cfg["ad"],)), max_size=REPLAY_ROWS, device=local, seed=101 + rank)
+    rb.fill_synthetic(REPLAY_ROWS, cfg["ma"], seed=7 + rank)
     if world > 1:
         uid = (C.c_ubyte * 128)()
         t = torch.zeros(128, dtype=torch.uint8, device="cuda")
@@ -173,11 +214,11 @@ def main():
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        pol.train(rb, BATCH)
+        pol.train(rb, B)
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        pol.train(rb, BATCH)
+        pol.train(rb, B)
     pol.sync()
     torch.cuda.synchronize()
     if dist is not None:
@@ -190,25 +231,28 @@ def main():
 
     rows, fam, roof = None, None, None
     if not args.no_roofline:           # every rank runs it: profiled steps contain collectives
-        rows = stage_table(pol, rb)
+        rows = stage_table(pol, rb, B, iters=50 if cfg["kind"] != "particles" else 3)
         if rank == 0:
             pmc = None
             pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc_path):
+            if os.path.exists(pmc_path) and args.config == "halfcheetah":
                 with open(pmc_path) as f:
                     pmc = json.load(f)
             roof, fam = roofline_from_stages(rows, pmc)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline()
+        cpu = cpu_baseline(cfg)
 
     if rank == 0:
         gsteps = args.steps / dt
         value = world * gsteps
+        metric = "TD3 gradient-steps/sec @ batch 256, HalfCheetah-v4, 1/2/4/8 GPU"
+        if args.config != "halfcheetah":
+            metric = f"TD3 gradient-steps/sec @ batch {B}, {args.config}, 1/2/4/8 GPU"
         out = {
-            "metric": "TD3 gradient-steps/sec @ batch 256, HalfCheetah-v4, 1/2/4/8 GPU",
-            "value": round(value, 2),
+            "metric": metric,
+            "value": round(value, 3),
             "unit": "grad-steps/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -218,14 +262,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (replay ring pre-filled on device: s,s' ~ N(0,1), a ~ U(-1,1), "
-                    "r ~ N(0,1), not_done ~ Bernoulli(0.99); torch-default random init)",
-            "config": {"workload": "TD3_featured.train(replay_buffer, 256) on HalfCheetah-v4 shapes "
-                                   "(state 17, action 6, actor 500-400-300, critic 2x 500-400-200, "
-                                   "LayerNorm, policy_freq 2), replay 1e6 per GPU",
-                       "global_batch": BATCH * world, "per_gpu_batch": BATCH, "replay_per_gpu": REPLAY,
+            "data": "synthetic (replay ring pre-filled on device: states / particles ~ N(0,1), "
+                    "a ~ U(-max_action, max_action), r ~ N(0,1), not_done ~ Bernoulli(0.99); "
+                    "torch-default random init)",
+            "config": {"workload": cfg["workload"],
+                       "global_batch": B * world, "per_gpu_batch": B, "replay_per_gpu": REPLAY_ROWS,
                        "parallelism": f"dp{world}" if world > 1 else "single",
-                       "global_steps_per_s": round(gsteps, 2),
+                       "global_steps_per_s": round(gsteps, 3),
                        "graph": not args.eager},
         }
         if roof is not None:
