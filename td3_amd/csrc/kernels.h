@@ -4,7 +4,14 @@
 #pragma once
 #include "common.h"
 
+#ifndef TD3_GEMM_WAVES
+#define TD3_GEMM_WAVES 8
+#endif
+
 namespace td3 {
+
+// Waves per GEMM-stage workgroup (K of a 32-row x 32*WN tile is split over kGemmWaves / WN waves).
+constexpr int kGemmWaves = TD3_GEMM_WAVES;
 
 // ------------------------------------------------------------------ batch-row GEMM stage
 // C[Bp x Nout] = epi( pro(A)[Bp x Kp] * B[Kp x Nout] )

@@ -38,7 +38,10 @@ __device__ __forceinline__ void lds_put_row(float* smem, int S, int row, int Kp,
 }
 
 // ================================================================== prologues
-// Each writes rows wave*8 .. wave*8+7 of the workgroup's A tile (LDS, [32][S]).
+// GEMM workgroups are kNW waves; each prologue writes rows wave*kRPW .. +kRPW-1 of the
+// workgroup's A tile (LDS, [32][S]).
+constexpr int kNW = kGemmWaves;
+constexpr int kRPW = 32 / kNW;
 struct Ctx {
   int m0, wave, lane, nt, Bp, S;
 };
@@ -46,22 +49,22 @@ struct Ctx {
 template <int RB>
 __device__ __forceinline__ void pro_copy(const GemmProb& P, float* smem, const Ctx& c) {
 #pragma unroll
-  for (int r0 = 0; r0 < 8; r0 += RB) {
+  for (int r0 = 0; r0 < kRPW; r0 += RB) {
     float x[RB][8];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
-      rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * 8 + r0 + r) * P.lda, P.Kp, c.lane);
+      rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r0 + r) * P.lda, P.Kp, c.lane);
 #pragma unroll
-    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * 8 + r0 + r, P.Kp, c.lane, x[r]);
+    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * kRPW + r0 + r, P.Kp, c.lane, x[r]);
   }
 }
 
 __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx& c) {
-  constexpr int RB = 8;
+  constexpr int RB = kRPW;
   float x[RB][8], g[8], bb[8], mean[RB], rstd[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r)
-    rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * 8 + r) * P.lda, P.Kp, c.lane);
+    rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r) * P.lda, P.Kp, c.lane);
   rv_load(g, P.lng, P.Kp, c.lane);
   rv_load(bb, P.lnb, P.Kp, c.lane);
 #if TD3_EXP == 1
@@ -72,7 +75,7 @@ __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx
   const bool t0 = c.nt == 0;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
-    const int row = c.wave * 8 + r, grow = c.m0 + row;
+    const int row = c.wave * kRPW + r, grow = c.m0 + row;
     lds_put_row(smem, c.S, row, P.Kp, c.lane, x[r]);
     if (t0 && P.Aout) rv_store(P.Aout + (size_t)grow * P.ldao, P.Kp, c.lane, x[r]);
     if (t0 && P.stats && c.lane == 0) {
@@ -88,11 +91,11 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
   rv_load(g, P.lng, P.Kp, c.lane);
   const bool t0 = c.nt == 0;
 #pragma unroll
-  for (int r0 = 0; r0 < 8; r0 += RB) {
+  for (int r0 = 0; r0 < kRPW; r0 += RB) {
     float gu[RB][8], h[RB][8], mean[RB], rstd[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const int grow = c.m0 + c.wave * 8 + r0 + r;
+      const int grow = c.m0 + c.wave * kRPW + r0 + r;
       rv_load(gu[r], P.A + (size_t)grow * P.lda, P.Kp, c.lane);
       rv_load(h[r], P.H + (size_t)grow * P.ldh, P.Kp, c.lane);
       mean[r] = P.norm ? gld(P.stats + (grow)) : 0.f;
@@ -101,7 +104,7 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
     ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.Kreal, c.lane, P.norm);
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const int row = c.wave * 8 + r0 + r;
+      const int row = c.wave * kRPW + r0 + r;
       lds_put_row(smem, c.S, row, P.Kp, c.lane, gu[r]);
       if (t0 && P.Aout) rv_store(P.Aout + (size_t)(c.m0 + row) * P.ldao, P.Kp, c.lane, gu[r]);
     }
@@ -531,7 +534,9 @@ __global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
 //  3. per chunk a lane reads 16 A values (4x ds_read_b128) and issues 16
 //     v_mfma_f32_32x32x2_f32 (lane half h supplies k = 16h + s of MFMA s),
 //  4. WK > 1: the partial tiles are summed through LDS; bias / ReLU epilogue.
-constexpr int kMaxChunks = 4;
+// With kNW waves, a wave holds at most 16 / kNW chunks of K <= 512 (WN = 1: WK = kNW;
+// WN = 4 only runs K <= 128 with WK = kNW / 4).
+constexpr int kMaxChunks = 16 / kNW;
 
 template <int MODE>
 __device__ __forceinline__ void load_b(const GemmProb& P, float (&bv)[kMaxChunks][16], int cb, int nch,
@@ -566,11 +571,13 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 }
 
 template <int MODE, int WN, int PRO>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmTable tab, int Bp, Counters* bump, int bump_actor,
-                                                      int nb) {
+__global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, Counters* bump, int bump_actor,
+                                                        int nb) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
-  constexpr int WK = 4 / WN;
+  constexpr int WK = kNW / WN;
+  constexpr int NT = 64 * kNW;                 // threads
+  constexpr int OUTW = 32 * WN;                // output columns of the workgroup
   constexpr bool kPrefetchB = true;
   const int b = xcd_tile(nb);
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -602,8 +609,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmTable tab, int Bp, Cou
 
   float bv[kMaxChunks][16];
   // bias of the epilogue's column, requested with the weights (off the tail of the chain)
-  const int bcol = (WK == 1) ? ncol : n0 + (threadIdx.x & 31);
-  const float bias = (MODE == 0 && P.bias && (WK > 1 || active)) ? gld(P.bias + bcol) : 0.f;
+  const int bcol = (WK == 1) ? ncol : n0 + (int)(threadIdx.x % OUTW);
+  const float bias = (MODE == 0 && P.bias && (WK > 1 ? bcol < P.Nout : active)) ? gld(P.bias + bcol) : 0.f;
   if constexpr (kPrefetchB) {
 #if TD3_EXP == 3
     for (int cc = 0; cc < kMaxChunks; ++cc) for (int q = 0; q < 16; ++q) bv[cc][q] = (float)(q + cc);
@@ -614,7 +621,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmTable tab, int Bp, Cou
   }
 
   const Ctx c{m0, wave, lane, nt, Bp, S};
-  if constexpr (PRO == kProCopy) pro_copy<8>(P, smem, c);
+  if constexpr (PRO == kProCopy) pro_copy<kRPW>(P, smem, c);
   else if constexpr (PRO == kProLN) pro_ln(P, smem, c);
   else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
   __syncthreads();
@@ -659,20 +666,21 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmTable tab, int Bp, Cou
     }
   } else {
     __syncthreads();
-    float* red = smem;  // [4][32][33]
+    float* red = smem;  // [kNW][32][33]; wave = wk * WN + wn
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = threadIdx.x + 256 * q;
-      const int row = e >> 5, col = e & 31;
-      float v = red[row * 33 + col];
+    for (int q = 0; q < 32 * OUTW / NT; ++q) {
+      const int e = threadIdx.x + NT * q;
+      const int row = e / OUTW, colw = e % OUTW;
+      const int wnn = colw >> 5, ci = colw & 31;
+      float v = red[(wnn * 32 + row) * 33 + ci];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) v = v + red[(w * 32 + row) * 33 + col];
+      for (int w = 1; w < WK; ++w) v = v + red[((w * WN + wnn) * 32 + row) * 33 + ci];
       if (MODE == 0 && P.bias) v = v + bias;
       if (P.relu) v = fmaxf(v, 0.f);
-      gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + col), v);
+      if (n0 + colw < P.Nout) gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + colw), v);
     }
   }
 }
@@ -879,7 +887,7 @@ __global__ __launch_bounds__(256) void polyak_flat_kernel(float* T, const float*
 template <int MODE, int WN, int PRO>
 static void gl(const GemmTable& t, int nblocks, int Bp, int lds, Counters* bump, int ba, hipStream_t s) {
   const int padded = (nblocks + 7) & ~7;
-  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(256), lds, s, t, Bp, bump, ba, nblocks);
+  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(64 * kNW), lds, s, t, Bp, bump, ba, nblocks);
 }
 
 using GemmFn = void (*)(const GemmTable&, int, int, int, Counters*, int, hipStream_t);

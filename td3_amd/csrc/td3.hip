@@ -272,7 +272,7 @@ static void alloc_eval(Scratch& S, const NetL& n, int Bp, float* X, int ldx, boo
 }
 
 static int gemm_lds_bytes(int Kp) {
-  int f = std::max(32 * lds_stride(Kp), 4 * 32 * 33);
+  int f = std::max(32 * lds_stride(Kp), kGemmWaves * 32 * 33);
   return f * 4;
 }
 
