@@ -307,14 +307,29 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
     rs0[0] = rs3[0] = 1.f;
   }
   const float tl = c.lane < ad ? gld(P.ex[5] + ((size_t)c.row * 32 + c.lane)) : 0.f;
+  // W1[:, sd+o]: the action columns of each W1 row the lane needs, as three float4 loads
+  // from the 16-B aligned column below sd (rows are contiguous; pads are zero)
+  {
+    const int sa = sd & ~3, so = sd & 3;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const float* wp = P.ex[4] + ((size_t)rcol(c.lane, jj) * ldw1 + sa);
+      float v[12];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const float4 t = gld4(wp + 4 * q);
+        v[4 * q + 0] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      }
+#pragma unroll
+      for (int o = 0; o < kHeadRegs; ++o) {
+        const float x = so == 0 ? v[o] : so == 1 ? v[o + 1] : so == 2 ? v[o + 2] : v[o + 3];
+        w1[o][jj] = o < ad ? x : 0.f;
+      }
+    }
+  }
 #pragma unroll
   for (int o = 0; o < kHeadRegs; ++o) {
     const int oo = o < ad ? o : 0;
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int n = rcol(c.lane, jj);
-      w1[o][jj] = gld(P.ex[4] + ((size_t)(n < K0 ? n : 0) * ldw1 + sd + oo));   // W1[:, sd+o]
-    }
     rv_load(w4[o], P.ex[6] + (size_t)oo * ldw4, ldw4, c.lane);
   }
   ln_bwd_rows<1>(gu0, h0, g0, mn0, rs0, K0, c.lane, P.norm);       // dZ0 of Q1 (pads -> 0)
