@@ -57,6 +57,7 @@ struct EncBwdProb {
   const float* gamma;               // lnorm1 weight
   int Kin;                          // real width of the MLP input row
   float* partial;                   // [nwg][EncOff::size(D)]
+  float* gpool;                     // [Bp][128] dz2 row scale: relu'(pooled) * dpooled / N
 };
 
 struct EncBwdArgs {

@@ -170,6 +170,35 @@ __device__ __forceinline__ int h1_at(int R, int k) { return R * kEncC1 + (k ^ ((
 // after unrolling, so LDS addresses are one lane base + an immediate offset per r.
 __device__ __forceinline__ constexpr int crow(int r) { return (r & 3) + 8 * (r >> 2); }
 
+// Pooled-feature grad of every batch row (one wave per row): LN_in backward of the MLP input
+// grad (no ReLU before lnorm1), then the pool ReLU (pooled > 0) and the 1/N of the mean.
+__global__ __launch_bounds__(256) void enc_gpool_kernel(EncBwdArgs a) {
+  const EncBwdProb& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.B) return;
+  float gu[1][8], xr[1][8], gm[8], mean[1], rstd[1];
+  rv_load(gu[0], P.GU + (size_t)b * P.ldgu, P.Kin, lane);
+  rv_load(xr[0], P.X + (size_t)b * P.ldx, P.Kin, lane);
+  if (P.stats) {
+    rv_load(gm, P.gamma, P.Kin, lane);
+    mean[0] = gld(P.stats + b);
+    rstd[0] = gld(P.stats + (a.Bp + b));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gm[j] = 1.f;
+    mean[0] = 0.f;
+    rstd[0] = 1.f;
+  }
+  ln_bwd_rows<1, false>(gu, xr, gm, mean, rstd, P.Kin, lane, P.stats ? 1 : 0);
+  const float invn = 1.0f / (float)a.N;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = rcol(lane, j);
+    if (c < kEncC2) gst(P.gpool + ((size_t)b * kEncC2 + c), xr[0][j] > 0.f ? gu[0][j] * invn : 0.f);
+  }
+}
+
 template <int DK, int ROLE>
 __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   extern __shared__ float4 sm4[];
@@ -217,45 +246,32 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
 
   const int g = blockIdx.x;
   const int b_begin = (int)((int64_t)g * a.B / a.nwg), b_end = (int)((int64_t)(g + 1) * a.B / a.nwg);
-  int tcount = 0;
-  for (int b = b_begin; b < b_end; ++b) {
-    const int sb = (b - b_begin) & 1;
-    float* gsb = gs + sb * kEncC2;
-    if (wave == 0) {
-      // pooled-feature grad: LN_in backward of this row (no ReLU before lnorm1), then the
-      // pool ReLU (pooled > 0) and the 1/N of the mean
-      float gu[1][8], xr[1][8], gm[8], mean[1], rstd[1];
-      rv_load(gu[0], P.GU + (size_t)b * P.ldgu, P.Kin, lane);
-      rv_load(xr[0], P.X + (size_t)b * P.ldx, P.Kin, lane);
-      if (P.stats) {
-        rv_load(gm, P.gamma, P.Kin, lane);
-        mean[0] = gld(P.stats + b);
-        rstd[0] = gld(P.stats + (a.Bp + b));
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gm[j] = 1.f;
-        mean[0] = 0.f;
-        rstd[0] = 1.f;
-      }
-      ln_bwd_rows<1, false>(gu, xr, gm, mean, rstd, P.Kin, lane, P.stats ? 1 : 0);
-      const float invn = 1.0f / (float)a.N;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = rcol(lane, j);
-        if (c < kEncC2) gsb[c] = xr[0][j] > 0.f ? gu[0][j] * invn : 0.f;
-      }
-    }
+  const int ntot = (b_end - b_begin) * a.ntile;
+  // staging of one tile: thread (row = tid>>4, d = tid&15) one particle coordinate, threads < 64
+  // one ReLU-bit word, threads < 128 one pooled-grad channel; tile it+1 is requested while
+  // tile it is multiplied
+  const int srow = tid >> 4, sd = tid & 15;
+  float st_x = 0.f, st_g = 0.f;
+  uint64_t st_m = 0;
+  auto fetch = [&](int it) {
+    const int b = b_begin + it / a.ntile, t = it % a.ntile;
     const float* base = a.data + (size_t)a.idx[b] * a.rec + P.part_off;
-    for (int t = 0; t < a.ntile; ++t, ++tcount) {
-      const int buf = tcount & 1;
-      float* xb = xs + buf * 32 * kEncMaxD;
-      uint64_t* mb = ms + buf * 64;
-      {
-        const int row = tid >> 4, d = tid & 15;
-        xb[row * kEncMaxD + d] = part_ld(base, t * 32 + row, a.N, D, d);
-        if (tid < 64) mb[tid] = *(const GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + tid);
-      }
-      __syncthreads();
+    st_x = part_ld(base, t * 32 + srow, a.N, D, sd);
+    if (tid < 64) st_m = *(const GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + tid);
+    if (tid < kEncC2) st_g = gld(P.gpool + ((size_t)b * kEncC2 + tid));
+  };
+  if (ntot > 0) fetch(0);
+  for (int it = 0; it < ntot; ++it) {
+    const int buf = it & 1;
+    float* xb = xs + buf * 32 * kEncMaxD;
+    uint64_t* mb = ms + buf * 64;
+    float* gsb = gs + buf * kEncC2;
+    xb[srow * kEncMaxD + sd] = st_x;
+    if (tid < 64) mb[tid] = st_m;
+    if (tid < kEncC2) gsb[tid] = st_g;
+    __syncthreads();
+    if (it + 1 < ntot) fetch(it + 1);
+    {
       if constexpr (ROLE == 0) {
         // ---- dh1 tile (rows i, channels k_own): A = dz2[row i][c], B = W2^T[k][c]
         f32x16 acc;
@@ -333,7 +349,6 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      __syncthreads();
     }
   }
   // ---- partial slab of this workgroup
@@ -400,6 +415,7 @@ int launch_enc_bwd(const EncBwdArgs& a, hipStream_t s) {
     set_error("launch_enc_bwd: D %d / nprob %d out of range", a.D, a.nprob);
     return -1;
   }
+  hipLaunchKernelGGL(enc_gpool_kernel, dim3((a.B + 3) / 4, a.nprob), dim3(256), 0, s, a);
   const dim3 grid(a.nwg, a.nprob);
 #define TD3_ENC_BWD(DK)                                                                        \
   hipLaunchKernelGGL((enc_bwd_kernel<DK, 0>), grid, dim3(512), enc_bwd_lds<0>(), s, a);       \

@@ -146,6 +146,7 @@ struct EvalB {
   float* GUin = nullptr;
   uint64_t* mask = nullptr;
   float* partial = nullptr;
+  float* gpool = nullptr;   // [Bp][128] pooled-feature grad rows of the encoder backward
 };
 
 struct Scratch {
@@ -886,6 +887,7 @@ static void push_enc_bwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const s
                     q.gamma = it.P + it.net->ln_in.offg;
                     q.Kin = it.net->lin[0].K;
                     q.partial = it.e->partial;
+                    q.gpool = it.e->gpool;
                   }
                   a.nprob = (int)items.size();
                   a.data = P->src_data;
@@ -947,7 +949,8 @@ static int build_step_particles(td3_handle* h, int B) {
   const size_t encsz = (size_t)EncOff::size(D);
   const size_t mask_f = (size_t)Bp * ntile * 64 * 2;
   size_t floats = (size_t)Bp * (2 * P->ld_a + 5 * P->ld_q) + 16 * (size_t)Bp + (size_t)Bp * ad +
-                  (size_t)Bp * 32 + (size_t)Bp * 2 * N * D + 3 * mask_f + 3 * P->nwg * encsz + 16384;
+                  (size_t)Bp * 32 + (size_t)Bp * 2 * N * D + 3 * mask_f + 3 * P->nwg * encsz +
+                  3 * (size_t)Bp * kEncC2 + 16384;
   floats += 2 * eval_floats(an, Bp, true, norm) + 6 * eval_floats(q1, Bp, true, norm);
   P->scratch_bytes = floats * sizeof(float);
   TD3_HIP(hipMalloc(&P->scratch, P->scratch_bytes));
@@ -980,6 +983,7 @@ static int build_step_particles(td3_handle* h, int B) {
     if (e == &P->Q[1] && !cdq) continue;
     e->mask = reinterpret_cast<uint64_t*>(S.take(mask_f));
     e->partial = S.take((size_t)P->nwg * encsz);
+    e->gpool = S.take((size_t)Bp * kEncC2);
   }
   if (S.used > S.cap) {
     set_error("internal: scratch overflow (%zu > %zu)", S.used, S.cap);
