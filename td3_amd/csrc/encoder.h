@@ -30,7 +30,11 @@ struct EncFwdProb {
   const float* enc;        // encoder parameter block (EncOff layout)
   int part_off;            // float offset of the [N][D] particle block inside a record
   float* out; int ldo;     // pooled features -> out[b * ldo + c], c < 128
-  uint64_t* mask;          // nullable: conv2 ReLU bits for the backward, [Bp][ntile][64] words
+  uint64_t* mask;          // nullable: ReLU bits for the backward: conv2 [Bp][ntile][64] words
+                           // (word j*16+r: channel tile j, MFMA reg r), then conv1
+                           // [Bp][ntile][2][64] words (half g, lane L: channels 32(4g+L/16)+L%16
+                           // low / +16 high, bit R = tile row R), then float counts of the
+                           // positive conv2 rows [Bp][128]
 };
 
 struct EncFwdArgs {
@@ -42,7 +46,8 @@ struct EncFwdArgs {
 };
 
 // ---------------------------------------------------------------- backward
-// Role A workgroups: dh1 = dz2 * W2 (MFMA), dz1 = relu'(z1) dh1, dW1 = dz1^T x (MFMA), db1.
+// Role A workgroups: dh1 = dz2 * W2 (MFMA), dz1 = relu'(z1) dh1 (the forward's conv1 bits),
+// dW1 = dz1^T x (MFMA), db1.
 // Role B workgroups: dW2 = dz2^T h1 (MFMA, h1 recomputed into LDS), db2 (mask popcounts).
 // dz2[n][c] = mask[n][c] * gpool[b][c] / N, gpool = relu'(pooled) * (LN_in backward of the MLP
 // input grad)[0..127].  Each workgroup owns a contiguous range of batch rows and writes its

@@ -4,10 +4,11 @@
 //                    conv2 (256->128) on v_mfma_f32_32x32x2_f32 with W2 staged once per
 //                    workgroup in LDS, ReLU, the mean over particles and the pool ReLU in the
 //                    epilogue (TD3_particles.py:52-58 / :103-109).  Neither h1 [B*N][256] nor
-//                    h2 [B*N][128] touches HBM: only the conv2 ReLU bits (1 bit per h2 element)
-//                    are kept for the backward.
-//   enc_bwd_kernel   the backward of the same, h1 recomputed from the particles: role A
-//                    workgroups form dh1 = dz2*W2 and dW1, db1; role B workgroups dW2 and db2.
+//                    h2 [B*N][128] touches HBM: only their ReLU bits (1 bit per element, from
+//                    wave ballots) are kept for the backward.
+//   enc_bwd_kernel   the backward of the same: role A workgroups form dh1 = dz2*W2 and dW1,
+//                    db1 (relu'(z1) from the conv1 bits); role B workgroups dW2 and db2 with h1
+//                    recomputed from the particles.
 //   enc_adam_kernel  fixed-order sum of the per-workgroup partial slabs, then torch Adam
 //                    (+ Polyak), or the grad arena on the all-reduced path.
 //
@@ -23,6 +24,17 @@ namespace td3 {
 // x tile rows of a batch row: rows r >= N read as zero.
 __device__ __forceinline__ float part_ld(const float* base, int n, int N, int D, int d) {
   return (n < N && d < D) ? gld(base + (size_t)n * D + d) : 0.f;
+}
+
+// v_writelane_b32: lane `lane` of `old` <- the uniform `val` (no builtin in this toolchain)
+__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t val, int lane) {
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "s"(lane) : "m0");
+  return old;
+}
+
+// lane L gets v when bit L of the uniform word m is set, else 0 (one v_cndmask on an SGPR pair)
+__device__ __forceinline__ float lane_select(uint64_t m, float v) {
+  return __builtin_amdgcn_inverse_ballot_w64(m) ? v : 0.f;
 }
 
 // ================================================================== forward
@@ -64,7 +76,9 @@ __global__ __launch_bounds__(512) void enc_fwd_kernel(EncFwdArgs a) {
     return;
   }
   const float* base = a.data + (size_t)a.idx[b] * a.rec + P.part_off;
+  uint64_t* mask1 = P.mask ? P.mask + (size_t)a.Bp * a.ntile * 64 : nullptr;
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
+  float npos[4] = {0.f, 0.f, 0.f, 0.f};                // rows with conv2 output > 0 (backward db2)
   for (int t = 0; t < a.ntile; ++t) {
     const int n = t * 32 + i;
     float x[DK];
@@ -75,6 +89,7 @@ __global__ __launch_bounds__(512) void enc_fwd_kernel(EncFwdArgs a) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    uint32_t m1lo = 0, m1hi = 0;
 #pragma unroll 1
     for (int c = 0; c < kEncC1 / 32; ++c) {
       // A operand: h1[n][k] = relu(b1[k] + sum_d W1[k][d] x[n][d]), k = 32c + 16h + s
@@ -100,6 +115,19 @@ __global__ __launch_bounds__(512) void enc_fwd_kernel(EncFwdArgs a) {
       }
 #pragma unroll
       for (int s = 0; s < 16; ++s) av[s] = fmaxf(av[s], 0.f);
+      if (mask1) {
+        // conv1 ReLU bits: ballot s of chunk c = rows of channels 32c+s (low) / 32c+16+s (high);
+        // lane (c&3)*16+s keeps it, and every 4 chunks the wave stores 64 words
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const uint64_t w = __ballot(av[s] > 0.f);
+          m1lo = writelane(m1lo, (uint32_t)w, (c & 3) * 16 + s);
+          m1hi = writelane(m1hi, (uint32_t)(w >> 32), (c & 3) * 16 + s);
+        }
+        if ((c & 3) == 3)
+          *(GAS uint64_t*)(mask1 + (((size_t)b * a.ntile + t) * 2 + (c >> 2)) * 64 + lane) =
+              ((uint64_t)m1hi << 32) | m1lo;
+      }
       // B operand: W2[j*32 + i][k]; conv2 output tile j (32 channels)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -115,7 +143,8 @@ __global__ __launch_bounds__(512) void enc_fwd_kernel(EncFwdArgs a) {
       }
     }
     // epilogue: bias, ReLU, row mask, column sums; one ReLU bit word per (channel tile, reg)
-    int wlo = 0, whi = 0;
+    // and the count of positive rows per channel
+    uint32_t wlo = 0, whi = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float bias = b2s[j * 32 + i];
@@ -127,35 +156,39 @@ __global__ __launch_bounds__(512) void enc_fwd_kernel(EncFwdArgs a) {
         part += v;
         if (P.mask) {
           const uint64_t w = __ballot(v > 0.f);           // uniform; lane j*16+r keeps it
-          const bool mine = lane == j * 16 + r;
-          wlo = mine ? (int)(uint32_t)w : wlo;
-          whi = mine ? (int)(uint32_t)(w >> 32) : whi;
+          wlo = writelane(wlo, (uint32_t)w, j * 16 + r);
+          whi = writelane(whi, (uint32_t)(w >> 32), j * 16 + r);
+          npos[j] += v > 0.f ? 1.f : 0.f;
         }
       }
       cs[j] += (double)part;
     }
-    if (P.mask) {
-      const uint64_t word = ((uint64_t)(uint32_t)whi << 32) | (uint32_t)wlo;
-      *(GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + lane) = word;
-    }
+    if (P.mask) *(GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + lane) = ((uint64_t)whi << 32) | wlo;
   }
   // lanes i and i + 32 hold the same channel (different rows): combine, mean, pool ReLU
+  float* cnt = P.mask ? reinterpret_cast<float*>(P.mask + (size_t)a.Bp * a.ntile * 192) : nullptr;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const double v = cs[j] + __shfl_xor(cs[j], 32, 64);
     if (h == 0) gst(P.out + ((size_t)b * P.ldo + j * 32 + i), fmaxf((float)(v / (double)a.N), 0.f));
+    if (cnt) {
+      const float c = npos[j] + __shfl_xor(npos[j], 32, 64);
+      if (h == 0) gst(cnt + ((size_t)b * kEncC2 + j * 32 + i), c);
+    }
   }
 }
 
 // ================================================================== backward
 constexpr int kEncS1 = 17;       // W1 [256][17] in LDS (odd stride: lane-indexed rows conflict-free)
 constexpr int kEncST = 132;      // W2^T [256][132] rows (== 4 mod 64)
-// role A stages W2^T [256][132]; role B the h1 tile [32][256]
+constexpr int kEncBufs = 2;      // staging double buffer: tile it+1 lands while tile it is used
+// role A stages W2^T [256][132]; role B keeps h1 in registers
+
 template <int ROLE>
-constexpr int enc_big() { return ROLE == 0 ? kEncC1 * kEncST : 32 * kEncC1; }
+constexpr int enc_big() { return ROLE == 0 ? kEncC1 * kEncST : 0; }
 template <int ROLE>
 constexpr int enc_bwd_lds() {
-  return (enc_big<ROLE>() + kEncC1 * kEncS1 + 2 * 32 * kEncMaxD + 2 * 64 * 2 + 2 * kEncC2 + kEncC1) * 4;
+  return (enc_big<ROLE>() + kEncC1 * kEncS1 + kEncBufs * (32 * kEncMaxD + 64 * 2 + kEncC2) + kEncC1) * 4;
 }
 static_assert(enc_bwd_lds<0>() <= 160 * 1024, "encoder backward LDS");
 
@@ -163,9 +196,6 @@ static_assert(enc_bwd_lds<0>() <= 160 * 1024, "encoder backward LDS");
 // mfma_row(r, lane); row R lives in word r = (R&3) + 4(R>>3), half (R>>2)&1.
 __device__ __forceinline__ int word_of_row(int R) { return (R & 3) + 4 * (R >> 3); }
 __device__ __forceinline__ int half_of_row(int R) { return (R >> 2) & 1; }
-// role B's h1 tile [32][256] in LDS, XOR-swizzled so the two lane halves (rows 4 apart) use
-// disjoint bank halves
-__device__ __forceinline__ int h1_at(int R, int k) { return R * kEncC1 + (k ^ (((R >> 2) & 1) << 5)); }
 // mfma_row(r, lane) = crow(r) + 4 * (lane >> 5): the r-dependent part is a compile-time constant
 // after unrolling, so LDS addresses are one lane base + an immediate offset per r.
 __device__ __forceinline__ constexpr int crow(int r) { return (r & 3) + 8 * (r >> 2); }
@@ -202,12 +232,12 @@ __global__ __launch_bounds__(256) void enc_gpool_kernel(EncBwdArgs a) {
 template <int DK, int ROLE>
 __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   extern __shared__ float4 sm4[];
-  float* big = reinterpret_cast<float*>(sm4);           // role A: W2^T [256][132]; role B: h1 [32][256]
+  float* big = reinterpret_cast<float*>(sm4);           // role A: W2^T [256][132]
   float* w1s = big + enc_big<ROLE>();                   // [256][17]
-  float* xs = w1s + kEncC1 * kEncS1;                    // [2][32][16]
-  uint64_t* ms = reinterpret_cast<uint64_t*>(xs + 2 * 32 * kEncMaxD);   // [2][64]
-  float* gs = reinterpret_cast<float*>(ms + 2 * 64);    // [2][128]
-  float* b1s = gs + 2 * kEncC2;                         // [256]
+  float* xs = w1s + kEncC1 * kEncS1;                    // [kEncBufs][32][16]
+  uint64_t* ms = reinterpret_cast<uint64_t*>(xs + kEncBufs * 32 * kEncMaxD);   // [kEncBufs][64]
+  float* gs = reinterpret_cast<float*>(ms + kEncBufs * 64);    // [kEncBufs][128]
+  float* b1s = gs + kEncBufs * kEncC2;                  // [256]
   const EncBwdProb& P = a.p[blockIdx.y];
   const int tid = threadIdx.x, D = a.D;
   const int wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
@@ -219,20 +249,24 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
       big[k * kEncST + c] = gld(W2 + e);
     }
   }
-  for (int e = tid; e < kEncC1 * kEncMaxD; e += 512) {
-    const int k = e >> 4, d = e & 15;
-    if (d < D) w1s[k * kEncS1 + d] = gld(W1 + k * D + d);
-    else if (d < kEncS1) w1s[k * kEncS1 + d] = 0.f;
+  if constexpr (ROLE == 1) {
+    for (int e = tid; e < kEncC1 * kEncMaxD; e += 512) {
+      const int k = e >> 4, d = e & 15;
+      if (d < D) w1s[k * kEncS1 + d] = gld(W1 + k * D + d);
+      else if (d < kEncS1) w1s[k * kEncS1 + d] = 0.f;
+    }
+    for (int e = tid; e < kEncC1; e += 512) b1s[e] = gld(P.enc + EncOff::b1(D) + e);
   }
-  for (int e = tid; e < kEncC1; e += 512) b1s[e] = gld(P.enc + EncOff::b1(D) + e);
   __syncthreads();
 
   const int k_own = wave * 32 + i;                      // this lane's conv1 channel (h1 tiles)
-  float w1r[DK];
+  float w1r[ROLE == 1 ? DK : 1];
+  float b1k = 0.f;
+  if constexpr (ROLE == 1) {
 #pragma unroll
-  for (int d = 0; d < DK; ++d) w1r[d] = w1s[k_own * kEncS1 + d];
-  const float b1k = b1s[k_own];
-  const int mt = wave & 3, kt0 = 4 * (wave >> 2);       // role B: dW2 tiles of this wave
+    for (int d = 0; d < DK; ++d) w1r[d] = w1s[k_own * kEncS1 + d];
+    b1k = b1s[k_own];
+  }
 
   f32x16 accW1;                                         // role A: dW1 tile
   f32x16 accB[ROLE == 1 ? 4 : 1];                       // role B: dW2 tiles
@@ -242,7 +276,7 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   for (int q = 0; q < (ROLE == 1 ? 4 : 1); ++q)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accB[q][r] = 0.f;
-  float gb1 = 0.f, gb2 = 0.f;
+  float gb1 = 0.f;
 
   const int g = blockIdx.x;
   const int b_begin = (int)((int64_t)g * a.B / a.nwg), b_end = (int)((int64_t)(g + 1) * a.B / a.nwg);
@@ -253,100 +287,118 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   const int srow = tid >> 4, sd = tid & 15;
   float st_x = 0.f, st_g = 0.f;
   uint64_t st_m = 0;
+  // role A: the forward's conv1 ReLU word of channel k_own (bit R = row R of the tile)
+  const uint64_t* mask1 = P.mask + (size_t)a.Bp * a.ntile * 64 + (wave >> 2) * 64 + (wave & 3) * 16 + (i & 15);
+  const int m1_sh = 32 * (i >> 4);
+  uint32_t st_r = 0;
   auto fetch = [&](int it) {
     const int b = b_begin + it / a.ntile, t = it % a.ntile;
     const float* base = a.data + (size_t)a.idx[b] * a.rec + P.part_off;
     st_x = part_ld(base, t * 32 + srow, a.N, D, sd);
-    if (tid < 64) st_m = *(const GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + tid);
+    if (ROLE == 0 && tid < 64) st_m = *(const GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + tid);
     if (tid < kEncC2) st_g = gld(P.gpool + ((size_t)b * kEncC2 + tid));
+    if constexpr (ROLE == 0) st_r = (uint32_t)(*(const GAS uint64_t*)(mask1 + ((size_t)b * a.ntile + t) * 128) >> m1_sh);
+  };
+  // ---- dh1 tile (rows i, channels k_own): A = dz2[row i][c], B = W2^T[k][c]
+  auto role_a_dh1 = [&](f32x16& ac, const uint64_t* mb, const float* gsb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ac[r] = 0.f;
+    const int wr = word_of_row(i), hr = half_of_row(i);
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const uint32_t bits = (uint32_t)(mb[cc * 16 + wr] >> (32 * hr)) >> (16 * h);
+      const float* gp = gsb + cc * 32 + 16 * h;
+      const float* wp = big + k_own * kEncST + cc * 32 + 16 * h;
+      float av[16], bv[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 gv = *reinterpret_cast<const float4*>(gp + 4 * q);
+        const float4 wv = *reinterpret_cast<const float4*>(wp + 4 * q);
+        av[4 * q + 0] = gv.x; av[4 * q + 1] = gv.y; av[4 * q + 2] = gv.z; av[4 * q + 3] = gv.w;
+        bv[4 * q + 0] = wv.x; bv[4 * q + 1] = wv.y; bv[4 * q + 2] = wv.z; bv[4 * q + 3] = wv.w;
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) av[s] = ((bits >> s) & 1u) ? av[s] : 0.f;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) ac = mfma32x32x2(av[s], bv[s], ac);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // ---- dz1 = relu'(z1) dh1 at (row mfma_row(r), channel k_own), relu'(z1) from the forward's
+  // conv1 bits (rb: bit R = tile row R); db1; dW1 += dz1^T x
+  auto role_a_dw1 = [&](const f32x16& ac, const float* xb, uint32_t rb) {
+    const float* xcol = xb + 4 * h * kEncMaxD + (i & 15);
+    rb >>= 4 * h;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float gz = ((rb >> crow(s)) & 1u) ? ac[s] : 0.f;
+      gb1 += gz;
+      const float xv = i < kEncMaxD ? xcol[crow(s) * kEncMaxD] : 0.f;
+      accW1 = mfma32x32x2(gz, xv, accW1);
+    }
   };
   if (ntot > 0) fetch(0);
   for (int it = 0; it < ntot; ++it) {
-    const int buf = it & 1;
+    const int buf = it % kEncBufs;
     float* xb = xs + buf * 32 * kEncMaxD;
     uint64_t* mb = ms + buf * 64;
     float* gsb = gs + buf * kEncC2;
     xb[srow * kEncMaxD + sd] = st_x;
-    if (tid < 64) mb[tid] = st_m;
+    if (ROLE == 0 && tid < 64) mb[tid] = st_m;
     if (tid < kEncC2) gsb[tid] = st_g;
+    const uint32_t rb_now = st_r;
     __syncthreads();
     if (it + 1 < ntot) fetch(it + 1);
     {
       if constexpr (ROLE == 0) {
-        // ---- dh1 tile (rows i, channels k_own): A = dz2[row i][c], B = W2^T[k][c]
         f32x16 acc;
+        role_a_dh1(acc, mb, gsb);
+        role_a_dw1(acc, xb, rb_now);
+      } else {
+        // ---- h1 of this wave's channels k_own at rows crow(r) + 4h, kept in registers as the
+        // B operand: lane (i, h) of step s supplies h1[row crow(s)+4h][k_own].
+        // A = dz2[row crow(s)+4h][mt*32 + i]: the forward's ballot word (mt, s) has bit
+        // i + 32h = lane for exactly that element, so one v_cndmask on the word (scalar
+        // loaded, one channel tile ahead) builds each operand
+        const uint64_t* mw = P.mask + ((size_t)(b_begin + it / a.ntile) * a.ntile + it % a.ntile) * 64;
+        uint64_t wq[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        const int wr = word_of_row(i), hr = half_of_row(i);
+        for (int s = 0; s < 16; ++s) wq[s] = mw[s];
+        __builtin_amdgcn_sched_barrier(0);
+        const float* xbase = xb + 4 * h * kEncMaxD;
+        float hv[16];
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          const uint32_t bits = (uint32_t)(mb[cc * 16 + wr] >> (32 * hr)) >> (16 * h);
-          const float* gp = gsb + cc * 32 + 16 * h;
-          const float* wp = big + k_own * kEncST + cc * 32 + 16 * h;
-          float av[16], bv[16];
+        for (int r0 = 0; r0 < 16; r0 += 4) {      // 4 rows at a time: independent FMA chains
+          float z[4], xv[4][DK];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float4 gv = *reinterpret_cast<const float4*>(gp + 4 * q);
-            const float4 wv = *reinterpret_cast<const float4*>(wp + 4 * q);
-            av[4 * q + 0] = gv.x; av[4 * q + 1] = gv.y; av[4 * q + 2] = gv.z; av[4 * q + 3] = gv.w;
-            bv[4 * q + 0] = wv.x; bv[4 * q + 1] = wv.y; bv[4 * q + 2] = wv.z; bv[4 * q + 3] = wv.w;
+            z[q] = b1k;
+#pragma unroll
+            for (int d = 0; d < DK; ++d) xv[q][d] = xbase[crow(r0 + q) * kEncMaxD + d];
           }
 #pragma unroll
-          for (int s = 0; s < 16; ++s) av[s] = ((bits >> s) & 1u) ? av[s] : 0.f;
+          for (int d = 0; d < DK; ++d)
 #pragma unroll
-          for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[s], acc);
+            for (int q = 0; q < 4; ++q) z[q] = __fmaf_rn(w1r[d], xv[q][d], z[q]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) hv[r0 + q] = fmaxf(z[q], 0.f);
           __builtin_amdgcn_sched_barrier(0);
         }
-        // ---- dz1 = relu'(z1) dh1 at (row mfma_row(r), channel k_own); db1; dW1 += dz1^T x
-        float gz1[16];
-        const float* xbase = xb + 4 * h * kEncMaxD;
+        // ---- dW2 tiles (conv2 channels mt*32 + m) x (conv1 channels k_own), K = the 32 rows
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float* xr = xbase + crow(r) * kEncMaxD;
-          float z = b1k;
+        for (int mt = 0; mt < 4; ++mt) {
+          uint64_t wn[16];
+          if (mt < 3)
 #pragma unroll
-          for (int d = 0; d < DK; ++d) z = __fmaf_rn(w1r[d], xr[d], z);
-          gz1[r] = z > 0.f ? acc[r] : 0.f;
-          gb1 += gz1[r];
-          __builtin_amdgcn_sched_barrier(0);   // one row of x at a time (VGPR budget)
-        }
-        const float* xcol = xbase + (i & 15);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const float xv = i < kEncMaxD ? xcol[crow(s) * kEncMaxD] : 0.f;
-          accW1 = mfma32x32x2(gz1[s], xv, accW1);
-        }
-      } else {
-        // ---- h1 tile into LDS (this wave: channels k_own of all 32 rows)
-        const float* xbase = xb + 4 * h * kEncMaxD;
-        float* hw = big + h1_at(4 * h, k_own);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float* xr = xbase + crow(r) * kEncMaxD;
-          float z = b1k;
-#pragma unroll
-          for (int d = 0; d < DK; ++d) z = __fmaf_rn(w1r[d], xr[d], z);
-          hw[crow(r) * kEncC1] = fmaxf(z, 0.f);
+            for (int s = 0; s < 16; ++s) wn[s] = mw[(mt + 1) * 16 + s];
+          const float gsc = gsb[mt * 32 + i];
           __builtin_amdgcn_sched_barrier(0);
-        }
-        __syncthreads();
-        // ---- dW2 tiles (channels c = mt*32 + i) x (conv1 channels kt*32 + i), K = the 32 rows
-        const float gsc = gsb[mt * 32 + i];
-        float av[16];
-        int cnt = 0;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const uint32_t bit = (uint32_t)(mb[mt * 16 + s] >> (i + 32 * h)) & 1u;
-          av[s] = bit ? gsc : 0.f;
-          cnt += (int)bit;
-        }
-        if (wave < 4) gb2 += gsc * (float)cnt;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float* hr = big + h1_at(4 * h, (kt0 + q) * 32 + i);
-#pragma unroll
-          for (int s = 0; s < 16; ++s) accB[q] = mfma32x32x2(av[s], hr[crow(s) * kEncC1], accB[q]);
+          for (int s = 0; s < 16; ++s) accB[mt] = mfma32x32x2(lane_select(wq[s], gsc), hv[s], accB[mt]);
           __builtin_amdgcn_sched_barrier(0);
+          if (mt < 3)
+#pragma unroll
+            for (int s = 0; s < 16; ++s) wq[s] = wn[s];
         }
       }
     }
@@ -366,11 +418,17 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int c = mt * 32 + mfma_row(r, lane), k = (kt0 + q) * 32 + i;
-        gst(out + (EncOff::w2(D) + (int64_t)c * kEncC1 + k), accB[q][r]);
+        const int c = q * 32 + mfma_row(r, lane);
+        gst(out + (EncOff::w2(D) + (int64_t)c * kEncC1 + k_own), accB[q][r]);
       }
-    const float v = gb2 + __shfl_xor(gb2, 32, 64);
-    if (wave < 4 && h == 0) gst(out + (EncOff::b2(D) + wave * 32 + i), v);
+    // db2[c] = sum over rows of dz2 = sum_b gpool[b][c] * (positive rows of channel c in b)
+    if (tid < kEncC2) {
+      const float* cnt = reinterpret_cast<const float*>(P.mask + (size_t)a.Bp * a.ntile * 192);
+      float gb2 = 0.f;
+      for (int b = b_begin; b < b_end; ++b)
+        gb2 = __fmaf_rn(gld(P.gpool + ((size_t)b * kEncC2 + tid)), gld(cnt + ((size_t)b * kEncC2 + tid)), gb2);
+      gst(out + (EncOff::b2(D) + tid), gb2);
+    }
   }
 }
 
@@ -379,8 +437,15 @@ __global__ __launch_bounds__(256) void enc_adam_kernel(EncAdamArgs a) {
   const EncAdamProb& P = a.p[blockIdx.y];
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= a.size) return;
-  float g = 0.f;
-  for (int w = 0; w < a.nwg; ++w) g += gld(P.partial + ((size_t)w * a.size + e));
+  // 8 independent partial sums (fixed order) keep 8 slab loads in flight per thread
+  float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float* src = P.partial + e;
+  int w = 0;
+  for (; w + 8 <= a.nwg; w += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ps[u] += gld(src + (size_t)(w + u) * a.size);
+  for (; w < a.nwg; ++w) ps[0] += gld(src + (size_t)w * a.size);
+  const float g = ((ps[0] + ps[1]) + (ps[2] + ps[3])) + ((ps[4] + ps[5]) + (ps[6] + ps[7]));
   const int64_t idx = P.off + e;
   if (a.mode == kDwGrad) {
     gst(a.adam.G + idx, g);

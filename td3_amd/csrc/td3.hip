@@ -197,7 +197,8 @@ struct Plan {
   int src_rec = 0, src_op = 0, src_op2 = 0;
   const int64_t* src_idx = nullptr;
   const void* src_key = nullptr;
-  int nwg = 0;                          // encoder-backward workgroups per role per network
+  int nwg = 0;                          // encoder-backward workgroups per role per critic network
+  int nwg_a = 0;                        // ... for the actor's encoder (one network per launch)
 };
 
 struct ActPlan {       // select_action / eval_q at small batch
@@ -865,6 +866,10 @@ static void push_enc_fwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const s
                 flops, "td3::enc_fwd_kernel<" + std::to_string(((D + 3) / 4) * 4) + ">"});
 }
 
+// One launch covers every network of a stage; its workgroups split the batch rows, 256 in all
+// (role A holds W2^T in LDS: one workgroup per CU).
+static int enc_bwd_nwg(int B, int nnets) { return std::max(1, std::min(B, 256 / std::max(1, nnets))); }
+
 static void push_enc_bwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const std::vector<BwdItem>& items,
                          const std::vector<float*>& X, const std::string& name) {
   const int N = h->N, D = h->D;
@@ -898,7 +903,7 @@ static void push_enc_bwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const s
                   a.N = N;
                   a.D = D;
                   a.ntile = (N + 31) / 32;
-                  a.nwg = P->nwg;
+                  a.nwg = enc_bwd_nwg(P->B, (int)items.size());
                   return launch_enc_bwd(a, s);
                 },
                 flops, "td3::enc_bwd_kernel<" + std::to_string(((D + 3) / 4) * 4) + ", 0>"});
@@ -944,12 +949,14 @@ static int build_step_particles(td3_handle* h, int B) {
   P->ldq = 32;
   P->ld_a = an.lin[0].Kp;
   P->ld_q = q1.lin[0].Kp;
-  P->nwg = std::max(1, std::min(B, 256 / nqn));
+  P->nwg = enc_bwd_nwg(B, nqn);
+  P->nwg_a = enc_bwd_nwg(B, 1);
   const int ntile = (N + 31) / 32;
   const size_t encsz = (size_t)EncOff::size(D);
   const size_t mask_f = (size_t)Bp * ntile * 64 * 2;
   size_t floats = (size_t)Bp * (2 * P->ld_a + 5 * P->ld_q) + 16 * (size_t)Bp + (size_t)Bp * ad +
-                  (size_t)Bp * 32 + (size_t)Bp * 2 * N * D + 3 * mask_f + 3 * P->nwg * encsz +
+                  (size_t)Bp * 32 + (size_t)Bp * 2 * N * D + 3 * (3 * mask_f + (size_t)Bp * kEncC2) +
+                  (2 * P->nwg + P->nwg_a) * encsz +
                   3 * (size_t)Bp * kEncC2 + 16384;
   floats += 2 * eval_floats(an, Bp, true, norm) + 6 * eval_floats(q1, Bp, true, norm);
   P->scratch_bytes = floats * sizeof(float);
@@ -981,8 +988,9 @@ static int build_step_particles(td3_handle* h, int B) {
   alloc_eval(S, q1, Bp, P->XAQ, P->ld_q, true, norm, true, P->AQ);
   for (EvalB* e : {&P->Q[0], &P->Q[1], &P->A}) {
     if (e == &P->Q[1] && !cdq) continue;
-    e->mask = reinterpret_cast<uint64_t*>(S.take(mask_f));
-    e->partial = S.take((size_t)P->nwg * encsz);
+    // conv2 words, conv1 words, positive-row counts [Bp][128] (EncFwdProb::mask)
+    e->mask = reinterpret_cast<uint64_t*>(S.take(3 * mask_f + (size_t)Bp * kEncC2));
+    e->partial = S.take((size_t)(e == &P->A ? P->nwg_a : P->nwg) * encsz);
     e->gpool = S.take((size_t)Bp * kEncC2);
   }
   if (S.used > S.cap) {
@@ -1176,7 +1184,7 @@ static int build_step_particles(td3_handle* h, int B) {
       std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
       TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true, true));
       push_enc_bwd(h, Pp, st, ab, {P->XA}, "AB_enc");
-      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, P->nwg));
+      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, P->nwg_a));
     }
   }
   if (h->plan) destroy_plan(h->plan.get());
