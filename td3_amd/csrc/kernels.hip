@@ -27,10 +27,6 @@
 #include "dev.h"
 #include "kernels.h"
 
-#ifndef TD3_EXP
-#define TD3_EXP 0   // timing experiments only (tools/): 1 no LN math, 2 no MFMA, 3 no weight loads
-#endif
-
 namespace td3 {
 
 __device__ __forceinline__ void lds_put_row(float* smem, int S, int row, int Kp, int lane, const float (&v)[8]) {
@@ -67,11 +63,7 @@ __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx
     rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r) * P.lda, P.Kp, c.lane);
   rv_load(g, P.lng, P.Kp, c.lane);
   rv_load(bb, P.lnb, P.Kp, c.lane);
-#if TD3_EXP == 1
-  for (int r = 0; r < RB; ++r) { mean[r] = g[0]; rstd[r] = bb[0]; }
-#else
   ln_fwd_rows<RB>(x, g, bb, P.Kreal, c.lane, mean, rstd);
-#endif
   const bool t0 = c.nt == 0;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
@@ -627,11 +619,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   const int bcol = (WK == 1) ? ncol : n0 + (int)(threadIdx.x % OUTW);
   const float bias = (MODE == 0 && P.bias && (WK > 1 ? bcol < P.Nout : active)) ? gld(P.bias + bcol) : 0.f;
   if constexpr (kPrefetchB) {
-#if TD3_EXP == 3
-    for (int cc = 0; cc < kMaxChunks; ++cc) for (int q = 0; q < 16; ++q) bv[cc][q] = (float)(q + cc);
-#else
     load_b<MODE>(P, bv, cb, nch, ncol, h);
-#endif
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
   }
 
@@ -656,13 +644,8 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
           const float4 v = *reinterpret_cast<const float4*>(arow + kb + 4 * q);
           av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
         }
-#if TD3_EXP == 2
-#pragma unroll
-        for (int s = 0; s < 16; ++s) acc[s] += av[s] * bv[cc][s];
-#else
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[cc][s], acc);
-#endif
       }
     }
   }

@@ -183,14 +183,14 @@ int rb_create_particles(int feat_dim, int n_particles, int particle_dim, int act
 int rb_destroy(rb_handle* h) {
   if (!h) return 0;
   Ring* r = reinterpret_cast<Ring*>(h);
-  hipSetDevice(r->device);
-  hipStreamSynchronize(r->stream);
-  hipFree(r->data);
-  hipFree(r->d_size);
-  hipFree(r->d_idx);
-  if (r->stage) hipHostFree(r->stage);
-  hipEventDestroy(r->stage_ev);
-  hipStreamDestroy(r->stream);
+  (void)hipSetDevice(r->device);
+  (void)hipStreamSynchronize(r->stream);
+  (void)hipFree(r->data);
+  (void)hipFree(r->d_size);
+  (void)hipFree(r->d_idx);
+  if (r->stage) (void)hipHostFree(r->stage);
+  (void)hipEventDestroy(r->stage_ev);
+  (void)hipStreamDestroy(r->stream);
   delete r;
   return 0;
 }

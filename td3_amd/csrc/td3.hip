@@ -584,7 +584,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
 }
 
 static void free_plan_tables(std::vector<void*>& t) {
-  for (void* p : t) hipFree(p);
+  for (void* p : t) (void)hipFree(p);
   t.clear();
 }
 
@@ -592,12 +592,12 @@ static void destroy_plan(Plan* p) {
   if (!p) return;
   for (int a = 0; a < 2; ++a) {
     for (int b = 0; b < 2; ++b) {
-      if (p->graph[a][b]) hipGraphExecDestroy(p->graph[a][b]);
-      if (p->graph_g[a][b]) hipGraphExecDestroy(p->graph_g[a][b]);
+      if (p->graph[a][b]) (void)hipGraphExecDestroy(p->graph[a][b]);
+      if (p->graph_g[a][b]) (void)hipGraphExecDestroy(p->graph_g[a][b]);
     }
   }
   free_plan_tables(p->tables);
-  if (p->scratch) hipFree(p->scratch);
+  if (p->scratch) (void)hipFree(p->scratch);
 }
 
 static size_t eval_floats(const NetL& n, int Bp, bool bwd, bool norm) {
@@ -912,8 +912,8 @@ static void push_enc_bwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const s
 static void destroy_graphs(Plan* P) {
   for (int a = 0; a < 2; ++a)
     for (int b = 0; b < 2; ++b) {
-      if (P->graph[a][b]) hipGraphExecDestroy(P->graph[a][b]);
-      if (P->graph_g[a][b]) hipGraphExecDestroy(P->graph_g[a][b]);
+      if (P->graph[a][b]) (void)hipGraphExecDestroy(P->graph[a][b]);
+      if (P->graph_g[a][b]) (void)hipGraphExecDestroy(P->graph_g[a][b]);
       P->graph[a][b] = P->graph_g[a][b] = nullptr;
     }
   P->graph_ring = nullptr;
@@ -1314,8 +1314,8 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(cs, &g);
     if (rc) {
-      if (g) hipGraphDestroy(g);
-      hipStreamDestroy(cs);
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipStreamDestroy(cs);
       return rc;
     }
     TD3_HIP(e);
@@ -1685,17 +1685,17 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
 
 int td3_destroy(td3_handle* h) {
   if (!h) return 0;
-  hipSetDevice(h->cfg.device);
-  hipStreamSynchronize(h->stream);
+  (void)hipSetDevice(h->cfg.device);
+  (void)hipStreamSynchronize(h->stream);
   if (h->plan) destroy_plan(h->plan.get());
   for (auto& kv : h->act) {
     free_plan_tables(kv.second->tables);
-    hipFree(kv.second->scratch);
+    (void)hipFree(kv.second->scratch);
   }
   if (h->comm) ncclCommDestroy(h->comm);
-  hipFree(h->arena);
-  hipFree(h->d_ctr);
-  hipStreamDestroy(h->stream);
+  (void)hipFree(h->arena);
+  (void)hipFree(h->d_ctr);
+  (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
 }
@@ -2065,7 +2065,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
       h->stage_kernels.push_back(st[i - 1].kernel);
     }
   }
-  for (auto& e : ev) hipEventDestroy(e);
+  for (auto& e : ev) (void)hipEventDestroy(e);
   *n_stages = n;
   h->last_body = &st;
   // the profiled step is a real step: keep the host mirror in sync
@@ -2109,8 +2109,8 @@ int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean) {
   float ms = 0;
   TD3_HIP(hipEventElapsedTime(&ms, a, b));
   *ms_mean = ms / iters;
-  hipEventDestroy(a);
-  hipEventDestroy(b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
   return 0;
 }
 
