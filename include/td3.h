@@ -58,6 +58,9 @@ int rb_create(int state_dim, int action_dim, int64_t max_size, int device, uint6
               rb_handle** out);
 int rb_destroy(rb_handle* h);
 int rb_info(const rb_handle* h, rb_info_t* info);
+/* The ring's own stream (hipStream_t): the stream a NULL `stream` argument selects.  Callers
+ * that consume rb_sample outputs on another stream order it after this one. */
+void* rb_stream(rb_handle* h);
 /* n transitions, row-major float64 host arrays (reference dtype); stores 1-done. */
 int rb_add(rb_handle* h, const double* state, const double* action, const double* next_state,
            const double* reward, const double* done, int64_t n, void* stream);

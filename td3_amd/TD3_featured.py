@@ -254,7 +254,11 @@ class TD3(TD3_base):
             raise ValueError("loading an optimizer with a different lr is not supported")
 
     def _stream(self):
-        return _torch().cuda.current_stream(self.device).cuda_stream
+        return None                      # the learner's own stream
+
+    def _torch_order(self):
+        from .my_replay_buffer import _TorchOrder
+        return _TorchOrder(self._lib.td3_stream(self._h), self.device)
 
     @property
     def total_it(self):
@@ -328,10 +332,13 @@ class TD3(TD3_base):
             torch = _torch()
             batch = replay_buffer.sample(B)
             ts = [torch.as_tensor(x, dtype=torch.float32).to(self.device).contiguous() for x in batch]
-            check(self._lib.td3_train_step_batch(self._h, *[t.data_ptr() for t in ts], B, self._stream(),
-                                                 _lib.fptr(nz) if nz is not None else None,
-                                                 C.byref(st) if st is not None else None),
-                  "td3_train_step_batch")
+            with self._torch_order() as ls:          # the batch was produced on torch's stream
+                for t in ts:
+                    t.record_stream(ls)
+                check(self._lib.td3_train_step_batch(self._h, *[t.data_ptr() for t in ts], B, self._stream(),
+                                                     _lib.fptr(nz) if nz is not None else None,
+                                                     C.byref(st) if st is not None else None),
+                      "td3_train_step_batch")
             keep.append(ts)
         if st is None:
             return None

@@ -197,10 +197,13 @@ class TD3(_FeaturedTD3):
             torch = _torch()
             batch = replay_buffer.sample(B)
             ts = [torch.as_tensor(x, dtype=torch.float32).to(self.device).contiguous() for x in batch]
-            check(self._lib.td3_train_step_batch_particles(
-                self._h, *[t.data_ptr() for t in ts], B, self._stream(),
-                _lib.fptr(nz) if nz is not None else None, C.byref(st) if st is not None else None),
-                "td3_train_step_batch_particles")
+            with self._torch_order() as ls:          # the batch was produced on torch's stream
+                for t in ts:
+                    t.record_stream(ls)
+                check(self._lib.td3_train_step_batch_particles(
+                    self._h, *[t.data_ptr() for t in ts], B, self._stream(),
+                    _lib.fptr(nz) if nz is not None else None, C.byref(st) if st is not None else None),
+                    "td3_train_step_batch_particles")
             keep.append(ts)
         if st is None:
             return None

@@ -49,6 +49,7 @@ SIGNATURES = {
     "rb_create": (C.c_int, [C.c_int, C.c_int, C.c_int64, C.c_int, C.c_uint64, C.POINTER(_P)]),
     "rb_destroy": (C.c_int, [_P]),
     "rb_info": (C.c_int, [_P, C.POINTER(rb_info_t)]),
+    "rb_stream": (_P, [_P]),
     "rb_add": (C.c_int, [_P, _D, _D, _D, _D, _D, C.c_int64, _P]),
     "rb_add_records": (C.c_int, [_P, _F, C.c_int64, _P]),
     "rb_fill_synthetic": (C.c_int, [_P, C.c_int64, C.c_float, C.c_uint64, _P]),

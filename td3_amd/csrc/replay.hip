@@ -131,6 +131,9 @@ static int ring_alloc(Ring* r, int64_t max_size, int device, uint64_t seed, rb_h
   TD3_HIP(hipMemset(r->data, 0, (size_t)max_size * r->rec * sizeof(float)));
   TD3_HIP(hipMalloc(&r->d_size, sizeof(int64_t)));
   TD3_HIP(hipMemset(r->d_size, 0, sizeof(int64_t)));
+  // the memsets ran on the null stream, which does not order the ring's non-blocking stream:
+  // finish them before any add / sample can be queued
+  TD3_HIP(hipDeviceSynchronize());
   TD3_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
   TD3_HIP(hipEventCreateWithFlags(&r->stage_ev, hipEventDisableTiming));
   *out = reinterpret_cast<rb_handle*>(r);
@@ -194,6 +197,8 @@ int rb_destroy(rb_handle* h) {
   delete r;
   return 0;
 }
+
+void* rb_stream(rb_handle* h) { return h ? (void*)reinterpret_cast<Ring*>(h)->stream : nullptr; }
 
 int rb_info(const rb_handle* h, rb_info_t* info) {
   TD3_ARG(h && info, "null handle");

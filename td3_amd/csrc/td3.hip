@@ -225,6 +225,11 @@ struct td3_handle {
   Counters* d_ctr = nullptr;
   int64_t total_it = 0, critic_step = 0, actor_step = 0;   // host mirror
   hipStream_t stream = nullptr;
+  // Acting path: select_action runs on its own stream and waits only for the
+  // last step that changed the online actor, so on critic-only steps (total_it % policy_freq != 0)
+  // it overlaps the training step instead of queueing behind it.
+  hipStream_t act_stream = nullptr;
+  hipEvent_t actor_ev = nullptr;              // recorded after every actor-updating step
   std::unique_ptr<Plan> plan;
   std::map<int, std::unique_ptr<ActPlan>> act;
   ncclComm_t comm = nullptr;
@@ -633,6 +638,7 @@ static int build_step(td3_handle* h, int B) {
   P->scratch_bytes = floats * sizeof(float);
   TD3_HIP(hipMalloc(&P->scratch, P->scratch_bytes));
   TD3_HIP(hipMemset(P->scratch, 0, P->scratch_bytes));
+  TD3_HIP(hipDeviceSynchronize());   // null-stream memset vs the non-blocking step stream
   Scratch S{P->scratch, floats, 0};
   P->X_S = S.take((size_t)Bp * P->ld_s);
   P->X_S2 = S.take((size_t)Bp * P->ld_s);
@@ -962,6 +968,7 @@ static int build_step_particles(td3_handle* h, int B) {
   P->scratch_bytes = floats * sizeof(float);
   TD3_HIP(hipMalloc(&P->scratch, P->scratch_bytes));
   TD3_HIP(hipMemset(P->scratch, 0, P->scratch_bytes));
+  TD3_HIP(hipDeviceSynchronize());   // null-stream memset vs the non-blocking step stream
   Scratch S{P->scratch, floats, 0};
   P->XA = S.take((size_t)Bp * P->ld_a);
   P->XTA = S.take((size_t)Bp * P->ld_a);
@@ -1348,7 +1355,10 @@ static void bind_ring(td3_handle* h, Ring* r) {
 static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_stats* stats) {
   h->total_it += 1;
   h->critic_step += 1;
-  if (actor_phase) h->actor_step += 1;
+  if (actor_phase) {
+    h->actor_step += 1;
+    TD3_HIP(hipEventRecord(h->actor_ev, s));
+  }
   if (!stats) return 0;
   Plan* P = h->plan.get();
   TD3_HIP(hipStreamSynchronize(s));
@@ -1402,6 +1412,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
                   2 * eval_floats(q1, Bp, false, norm) + 4096;
   TD3_HIP(hipMalloc(&A->scratch, floats * 4));
   TD3_HIP(hipMemset(A->scratch, 0, floats * 4));
+  TD3_HIP(hipDeviceSynchronize());
   Scratch S{A->scratch, floats, 0};
   A->X_S = S.take((size_t)Bp * lds_s);
   A->X_SA = S.take((size_t)Bp * lds_sa);
@@ -1486,6 +1497,7 @@ static int build_act_particles(td3_handle* h, int Bp, ActPlan** out) {
                   eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, false, norm) + 8192;
   TD3_HIP(hipMalloc(&A->scratch, floats * 4));
   TD3_HIP(hipMemset(A->scratch, 0, floats * 4));
+  TD3_HIP(hipDeviceSynchronize());
   Scratch S{A->scratch, floats, 0};
   A->X_S = S.take((size_t)Bp * lda);
   A->X_SA = S.take((size_t)Bp * ldq);
@@ -1678,7 +1690,10 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   }
   TD3_HIP(hipMalloc(&h->d_ctr, sizeof(Counters)));
   TD3_HIP(hipMemset(h->d_ctr, 0, sizeof(Counters)));
+  TD3_HIP(hipDeviceSynchronize());          // null-stream memsets vs the handle's non-blocking streams
   TD3_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  TD3_HIP(hipStreamCreateWithFlags(&h->act_stream, hipStreamNonBlocking));
+  TD3_HIP(hipEventCreateWithFlags(&h->actor_ev, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -1695,6 +1710,9 @@ int td3_destroy(td3_handle* h) {
   if (h->comm) ncclCommDestroy(h->comm);
   (void)hipFree(h->arena);
   (void)hipFree(h->d_ctr);
+  (void)hipStreamSynchronize(h->act_stream);
+  (void)hipStreamDestroy(h->act_stream);
+  (void)hipEventDestroy(h->actor_ev);
   (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -1872,7 +1890,8 @@ int td3_select_action(td3_handle* h, const float* state, float* action_out, int 
   TD3_HIP(hipSetDevice(h->cfg.device));
   ActPlan* A;
   TD3_RC(build_act(h, pad32(n), &A));
-  hipStream_t s = h->stream;
+  hipStream_t s = h->act_stream;
+  TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
   TD3_RC(copy_rows_h2d(A->X_S, pad32(h->sd), 0, state, n, h->sd, s));
   TD3_RC(run_stages(A->act, s));
   TD3_HIP(hipMemcpy2DAsync(action_out, (size_t)h->ad * 4, A->X_SP + h->sd, (size_t)pad32(h->sd + h->ad) * 4,
@@ -1948,7 +1967,8 @@ int td3_select_action_particles(td3_handle* h, const float* feat, const float* p
   TD3_HIP(hipSetDevice(h->cfg.device));
   ActPlan* A;
   TD3_RC(build_act_particles(h, pad32(n), &A));
-  hipStream_t s = h->stream;
+  hipStream_t s = h->act_stream;
+  TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
   const int np = h->N * h->D;
   const NetL& an = h->actor.nets[0];
   TD3_RC(copy_rows_h2d(A->X_S, an.lin[0].Kp, kEncC2, feat, n, h->sd, s));
@@ -2071,7 +2091,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   // the profiled step is a real step: keep the host mirror in sync
   h->total_it += 1;
   h->critic_step += 1;
-  if (actor_phase) h->actor_step += 1;
+  if (actor_phase) h->actor_step += 1;   // (stream synchronised above: no actor event needed)
   return 0;
 }
 

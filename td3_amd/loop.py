@@ -1,0 +1,150 @@
+"""The acting / training loop around the learner.
+
+``TrainLoop.run`` keeps the order of the reference's main loop (``main.py:240-289``): act
+(uniform random before ``start_policy``, else ``select_action`` + OU noise, clipped), ``env.step``,
+``add_to_replay_buffer`` (the transition and its hindsight relabels), then one ``policy.train``
+per environment step once ``t >= start_training``; episode ends reset the env and the noise.
+
+What runs where on MI355X:
+
+* ``policy.train`` only enqueues the captured step graph (no host sync), so ``env.step`` of the
+  next iteration runs on the host while the GPU trains;
+* ``select_action`` runs on the learner's acting stream and waits only for the last step that
+  changed the online actor (``td3_handle::actor_ev``).  On critic-only steps
+  (``total_it % policy_freq != 0``) it therefore overlaps the training step, and its result is
+  still exactly the sequential one: the actor it reads is the same;
+* ``add_to_replay_buffer`` hands the transition and all its relabels to the ring in one batched
+  ``rb_add`` (pinned staging, async copy on the ring's stream; ``train`` waits on its event), the
+  env-specific reward / state hooks staying on the host (``main.py:70-91``).
+
+The gym / MuJoCo / SPlisHSPlasH environments are not part of this build (not installed here);
+``SyntheticEnv`` is a gym-shaped stand-in with a configurable host cost per step, used by
+``bench.py --loop`` and the tests.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from .exploration import OrnsteinUhlenbeckActionNoise
+
+__all__ = ["add_to_replay_buffer", "TrainLoop", "SyntheticEnv", "Box"]
+
+
+def add_to_replay_buffer(replay_buffer, state, action, reward, next_state, done_bool, relabels=()):
+    """``main.py:70-91``: store the transition, then every hindsight relabel
+    ``(manip_state, manip_next_state, manip_reward)`` computed by the env hooks, as one batch."""
+    relabels = list(relabels)
+    if not relabels:
+        replay_buffer.add(state, action, next_state, reward, done_bool)
+        return
+    n = 1 + len(relabels)
+    s = np.stack([np.asarray(state, np.float64)] + [np.asarray(m[0], np.float64) for m in relabels])
+    s2 = np.stack([np.asarray(next_state, np.float64)] + [np.asarray(m[1], np.float64) for m in relabels])
+    r = np.array([float(reward)] + [float(m[2]) for m in relabels], np.float64)
+    a = np.repeat(np.asarray(action, np.float64).reshape(1, -1), n, axis=0)
+    d = np.full(n, float(done_bool), np.float64)
+    replay_buffer.add_batch(s, a, s2, r, d)
+
+
+class Box:
+    """The part of ``gym.spaces.Box`` the loop and the learners use: ``shape``, ``low``/``high``
+    and ``sample()`` (uniform, numpy's global RNG)."""
+
+    def __init__(self, low, high, shape):
+        self.shape = tuple(shape)
+        self.low = np.full(self.shape, low, np.float64)
+        self.high = np.full(self.shape, high, np.float64)
+
+    def sample(self):
+        return np.random.uniform(self.low, self.high)
+
+
+class SyntheticEnv:
+    """Gym-shaped stand-in: s' = tanh(W s + U a), r = -|s'|^2 / sd, episodes of fixed length.
+    ``step_cost_us`` busy-waits to model a simulator's host time per step."""
+
+    def __init__(self, state_dim, action_dim, max_action=1.0, max_episode_steps=1000, step_cost_us=0.0,
+                 seed=0):
+        rs = np.random.RandomState(seed)
+        self.observation_space = Box(-np.inf, np.inf, (state_dim,))
+        self.action_space = Box(-max_action, max_action, (action_dim,))
+        self._W = rs.standard_normal((state_dim, state_dim)) / np.sqrt(state_dim)
+        self._U = rs.standard_normal((state_dim, action_dim)) / np.sqrt(action_dim)
+        self._max_episode_steps = int(max_episode_steps)
+        self._cost = float(step_cost_us) * 1e-6
+        self._rs = rs
+        self._t = 0
+        self._s = None
+
+    def reset(self):
+        self._t = 0
+        self._s = self._rs.standard_normal(self.observation_space.shape[0]) * 0.1
+        return self._s.copy()
+
+    def step(self, action):
+        t0 = time.perf_counter()
+        a = np.asarray(action, np.float64).reshape(-1)
+        self._s = np.tanh(self._W @ self._s + self._U @ a)
+        self._t += 1
+        r = -float(self._s @ self._s) / len(self._s)
+        done = self._t >= self._max_episode_steps
+        while self._cost and time.perf_counter() - t0 < self._cost:
+            pass
+        return self._s.copy(), r, done, {}
+
+
+class TrainLoop:
+    """``main.py:240-289`` without evaluation, checkpoints and the RTPT progress bar (out of
+    scope); ``relabel(env, state, action, reward, next_state, done_bool)`` may return hindsight
+    relabels for ``add_to_replay_buffer``; ``on_episode_end(info)`` is called at episode ends."""
+
+    def __init__(self, env, policy, replay_buffer, *, max_action, start_policy=0, start_training=0,
+                 batch_size=256, expl_noise=0.1, done_swap=True, relabel=None, on_episode_end=None):
+        self.env, self.policy, self.replay_buffer = env, policy, replay_buffer
+        self.max_action = max_action
+        self.start_policy, self.start_training = int(start_policy), int(start_training)
+        self.batch_size = int(batch_size)
+        self.noise = OrnsteinUhlenbeckActionNoise(env.action_space.shape[0], sigma=expl_noise)
+        self.done_swap = done_swap
+        self.relabel = relabel
+        self.on_episode_end = on_episode_end
+
+    def run(self, max_timesteps):
+        env, policy, rb = self.env, self.policy, self.replay_buffer
+        state, done = env.reset(), False
+        episode_reward, episode_timesteps, episode_num, grad_steps = 0.0, 0, 0, 0
+        t0 = time.perf_counter()
+        for t in range(int(max_timesteps)):
+            episode_timesteps += 1
+            if t < self.start_policy:
+                action = env.action_space.sample()
+            else:
+                action = (policy.select_action(state) + self.noise.sample()).clip(-self.max_action,
+                                                                                  self.max_action)
+            next_state, reward, done, _ = env.step(action)
+            if self.done_swap:
+                done_bool = float(done) if episode_timesteps < env._max_episode_steps else 0.0
+            else:
+                done_bool = float(done)
+            relabels = self.relabel(env, state, action, reward, next_state, done_bool) if self.relabel else ()
+            add_to_replay_buffer(rb, state, action, reward, next_state, done_bool, relabels)
+            state = next_state
+            episode_reward += reward
+            if t >= self.start_training:
+                policy.train(rb, self.batch_size)
+                grad_steps += 1
+            if done:
+                if self.on_episode_end:
+                    self.on_episode_end({"t": t, "episode": episode_num, "reward": episode_reward,
+                                         "length": episode_timesteps})
+                state, done = env.reset(), False
+                self.noise.reset()
+                episode_reward, episode_timesteps = 0.0, 0
+                episode_num += 1
+        if hasattr(policy, "sync"):
+            policy.sync()
+        dt = time.perf_counter() - t0
+        return {"env_steps": int(max_timesteps), "grad_steps": grad_steps, "episodes": episode_num,
+                "seconds": dt, "env_steps_per_s": int(max_timesteps) / dt if dt > 0 else 0.0}

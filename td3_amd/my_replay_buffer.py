@@ -48,6 +48,25 @@ class _SafeIntUnpickler(pickle.Unpickler):
         raise pickle.UnpicklingError(f"refusing to load {module}.{name} from a buffer file")
 
 
+class _TorchOrder:
+    """Orders work on one of the library's non-blocking streams against torch's current stream:
+    on entry the library stream waits for torch's (tensors it reads or fills were made there),
+    on exit torch's stream waits for the library's (its outputs are then safe to use)."""
+
+    def __init__(self, stream_ptr, device):
+        torch = _torch()
+        self._torch_s = torch.cuda.current_stream(device)
+        self._lib_s = torch.cuda.ExternalStream(int(stream_ptr), device=device)
+
+    def __enter__(self):
+        self._lib_s.wait_stream(self._torch_s)
+        return self._lib_s
+
+    def __exit__(self, *exc):
+        self._torch_s.wait_stream(self._lib_s)
+        return False
+
+
 def _load_int(path):
     with open(path, "rb") as f:
         v = _SafeIntUnpickler(f).load()
@@ -112,8 +131,10 @@ class ReplayBuffer_featured(object):
         return int(self._info().size)
 
     def _stream(self):
-        torch = _torch()
-        return torch.cuda.current_stream(self.device).cuda_stream
+        return None                      # the ring's own stream (see _torch_order)
+
+    def _torch_order(self):
+        return _TorchOrder(self._lib.rb_stream(self._h), self.device)
 
     # ------------------------------------------------------------------ reference API
     def add(self, state, action, next_state, reward, done):
@@ -177,9 +198,10 @@ class ReplayBuffer_featured(object):
             size = self.size
             if B and (int(inj.min()) < 0 or int(inj.max()) >= max(size, 1)):
                 raise IndexError("index out of range of the filled buffer")
-        check(self._lib.rb_sample(self._h, B, *[t.data_ptr() for t in out],
-                                  inj.data_ptr() if inj is not None else None,
-                                  idx_out.data_ptr(), self._stream()), "rb_sample")
+        with self._torch_order():
+            check(self._lib.rb_sample(self._h, B, *[t.data_ptr() for t in out],
+                                      inj.data_ptr() if inj is not None else None,
+                                      idx_out.data_ptr(), self._stream()), "rb_sample")
         if return_indices:
             return out, idx_out
         return out
@@ -308,7 +330,10 @@ class ReplayBuffer_particles(object):
         return int(self._info().size)
 
     def _stream(self):
-        return _torch().cuda.current_stream(self.device).cuda_stream
+        return None
+
+    def _torch_order(self):
+        return _TorchOrder(self._lib.rb_stream(self._h), self.device)
 
     def _np(self):
         return self.n_particles * self.particle_dim
@@ -376,9 +401,10 @@ class ReplayBuffer_particles(object):
             size = self.size
             if B and (int(inj.min()) < 0 or int(inj.max()) >= max(size, 1)):
                 raise IndexError("index out of range of the filled buffer")
-        check(self._lib.rb_sample_particles(self._h, B, *[t.data_ptr() for t in out],
-                                            inj.data_ptr() if inj is not None else None,
-                                            idx_out.data_ptr(), self._stream()), "rb_sample_particles")
+        with self._torch_order():
+            check(self._lib.rb_sample_particles(self._h, B, *[t.data_ptr() for t in out],
+                                                inj.data_ptr() if inj is not None else None,
+                                                idx_out.data_ptr(), self._stream()), "rb_sample_particles")
         if return_indices:
             return out, idx_out
         return out

@@ -1,0 +1,66 @@
+"""Acting path on the MI355X.
+
+select_action runs on the learner's acting stream and waits only for the last actor update;
+on critic-only steps it overlaps the training step.  Its results must be exactly the
+sequential ones (the actor it reads is the same), which these tests check against a learner
+that synchronises after every step, and against the oracle's actor forward.
+"""
+import numpy as np
+import pytest
+
+from helpers import orc, featured_setup
+from test_gpu_parity import _make
+
+pytestmark = pytest.mark.gpu
+
+
+def test_select_action_overlap_equals_sequential():
+    S = featured_setup("hc_layer")
+    a, rb = _make(S)
+    b, _ = _make(S)
+    rs = np.random.RandomState(9)
+    states = rs.standard_normal((12, S["sd"])).astype(np.float32)
+    for t in range(12):
+        xa = a.select_action(states[t])          # may run while a's previous step trains
+        xb = b.select_action(states[t])
+        np.testing.assert_array_equal(xa, xb, err_msg=f"t={t}")
+        a.train(rb, S["B"])                      # async: returns after enqueueing the graph
+        b.train(rb, S["B"])
+        b.sync()
+    a.sync()
+    ref = orc.featured_select_action(a.actor.numpy_dict(), S["norm"], S["ma"], states[:1])
+    np.testing.assert_allclose(a.select_action(states[0]), np.asarray(ref).reshape(-1), rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(a.actor.flat(), b.actor.flat())
+    np.testing.assert_array_equal(a.critic.flat(), b.critic.flat())
+
+
+def test_select_action_sees_the_actor_update():
+    """After an actor step, select_action reflects the new actor (no stale read)."""
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    s = np.random.RandomState(4).standard_normal(S["sd"]).astype(np.float32)
+    before = pol.select_action(s)
+    pol.train(rb, S["B"])                        # total_it 1: critic only
+    assert np.array_equal(pol.select_action(s), before)
+    pol.train(rb, S["B"])                        # total_it 2: actor update
+    after = pol.select_action(s)
+    assert not np.array_equal(after, before)
+    pol.sync()
+    ref = orc.featured_select_action(pol.actor.numpy_dict(), S["norm"], S["ma"], s[None])
+    np.testing.assert_allclose(after, np.asarray(ref).reshape(-1), rtol=1e-5, atol=1e-6)
+
+
+def test_train_loop_runs_on_gpu():
+    from td3_amd.TD3_featured import TD3
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+    from td3_amd.loop import SyntheticEnv, TrainLoop
+    np.random.seed(0)
+    env = SyntheticEnv(17, 6, max_action=1.0, max_episode_steps=50)
+    pol = TD3(env.observation_space, env.action_space, max_action=1.0, norm="layer")
+    rb = ReplayBuffer_featured(env.observation_space, env.action_space, max_size=10_000)
+    loop = TrainLoop(env, pol, rb, max_action=1.0, start_policy=20, start_training=64, batch_size=64,
+                     relabel=lambda e, s, a, r, s2, d: [(s * 0.5, s2 * 0.5, r - 1.0)])
+    out = loop.run(200)
+    assert out["grad_steps"] == 136 and out["episodes"] == 4
+    assert rb.size == 400 and pol.total_it == 136
+    assert np.isfinite(pol.actor.flat()).all() and np.isfinite(pol.critic.flat()).all()
