@@ -546,25 +546,27 @@ __global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
 constexpr int kMaxChunks = 16 / kNW;
 
 template <int MODE>
+__device__ __forceinline__ void load_chunk(const GemmProb& P, float (&b)[16], int ch, int ncol, int h) {
+  const int kb = ch * 32 + 16 * h;
+  if (MODE == 0) {
+    const float* wp = P.W + (size_t)ncol * P.ldw + kb;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = gld4(wp + 4 * q);
+      b[4 * q + 0] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+    }
+  } else {
+    const float* wp = P.W + (size_t)kb * P.ldw + ncol;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) b[s] = gld(wp + (size_t)s * P.ldw);
+  }
+}
+
+template <int MODE>
 __device__ __forceinline__ void load_b(const GemmProb& P, float (&bv)[kMaxChunks][16], int cb, int nch,
                                        int ncol, int h) {
 #pragma unroll
-  for (int cc = 0; cc < kMaxChunks; ++cc) {
-    const int ch = min(cb + cc, nch - 1);
-    const int kb = ch * 32 + 16 * h;
-    if (MODE == 0) {
-      const float* wp = P.W + (size_t)ncol * P.ldw + kb;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = gld4(wp + 4 * q);
-        bv[cc][4 * q + 0] = v.x; bv[cc][4 * q + 1] = v.y; bv[cc][4 * q + 2] = v.z; bv[cc][4 * q + 3] = v.w;
-      }
-    } else {
-      const float* wp = P.W + (size_t)kb * P.ldw + ncol;
-#pragma unroll
-      for (int s = 0; s < 16; ++s) bv[cc][s] = gld(wp + (size_t)s * P.ldw);
-    }
-  }
+  for (int cc = 0; cc < kMaxChunks; ++cc) load_chunk<MODE>(P, bv[cc], min(cb + cc, nch - 1), ncol, h);
 }
 
 // XCD-aware tile order (cdna_hip_programming.md §5.5 T1): the dispatcher deals blocks
@@ -646,6 +648,25 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
         }
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[cc][s], acc);
+      }
+    }
+    // WN=4 on a wide K leaves this wave more than kMaxChunks chunks: the rest are streamed, the
+    // weights of chunk ch+1 in flight while chunk ch is multiplied
+    if (cb + kMaxChunks < ce) {
+      float bn[16];
+      load_chunk<MODE>(P, bn, cb + kMaxChunks, ncol, h);
+      for (int ch = cb + kMaxChunks; ch < ce; ++ch) {
+        float bc[16], av[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bc[s] = bn[s];
+        if (ch + 1 < ce) load_chunk<MODE>(P, bn, ch + 1, ncol, h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(arow + ch * 32 + 4 * q);
+          av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bc[s], acc);
       }
     }
   }

@@ -320,6 +320,16 @@ static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<
   return 0;
 }
 
+// Output columns per GEMM workgroup.  32 (WN=1, K split 8 ways) gives the shortest MFMA chain:
+// right for the latency-bound B=256 stages (WN=4 there measured slower: HalfCheetah F_fwd1
+// 14.8 -> 18.3 us).  At B >= 512 a stage of >= 256 such workgroups is bound by the A rows and
+// weights every 32-column tile re-reads; 128 columns per workgroup (WN=4, K split 2 ways, wide K
+// streamed chunk by chunk) cut that traffic: Humanoid B=1024 2.70k -> 2.92k steps/s, particles
+// B=4096 MLP stages -20 %.  Narrow K (<= 128) always uses WN=4.
+static int gemm_wn(int maxK, int Bp, int wn1_blocks) {
+  return (maxK <= 128 || (Bp >= 512 && wn1_blocks >= 256)) ? 4 : 1;
+}
+
 // Forward layers 0..2 of several networks (one launch per layer); layer 0 copies the
 // network input rows, layers 1 and 2 apply the previous layer's LayerNorm in the prologue.
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
@@ -329,8 +339,12 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
   for (int l = 0; l < 3; ++l) {
     std::vector<GemmProb> probs;
     int maxKp = 0;
-    for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Kp);
-    const int wn = maxKp <= 128 ? 4 : 1;
+    int wn1_blocks = 0;
+    for (auto& it : items) {
+      maxKp = std::max(maxKp, it.net->lin[l].Kp);
+      wn1_blocks += (Bp / 32) * ((it.net->lin[l].Np + 31) / 32);
+    }
+    const int wn = gemm_wn(maxKp, Bp, wn1_blocks);
     const bool lnin = items[0].net->lnin;          // TD3_particles lnorm1 on the MLP input
     const int pro = l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
     int blocks = 0, lds = 0;
@@ -402,8 +416,12 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     int blocks = 0, lds = 0;
     double flops = 0;
     int maxKp = 0;
-    for (auto& it : items) maxKp = std::max(maxKp, it.net->lin[l].Np);
-    const int wn = maxKp <= 128 ? 4 : 1;
+    int wn1_blocks = 0;
+    for (auto& it : items) {
+      maxKp = std::max(maxKp, it.net->lin[l].Np);
+      wn1_blocks += (Bp / 32) * ((it.net->lin[l].Kp + 31) / 32);
+    }
+    const int wn = gemm_wn(maxKp, Bp, wn1_blocks);
     for (size_t k = 0; k < items.size(); ++k) {
       const BwdItem& it = items[k];
       const LinearL& L = it.net->lin[l];

@@ -250,3 +250,29 @@ def test_allreduce_path_single_rank():
         _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (p, "actor"))
         _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"))
         _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"))
+
+
+@pytest.mark.parametrize("B", [512, 1024])
+def test_large_batch_teacher_forced(B):
+    """Batches >= 512 switch the wide stages to 128-column GEMM workgroups with the K chunks
+    streamed (td3.hip gemm_wn): a critic-only and an actor step against the oracle."""
+    S = featured_setup("hc_layer")
+    S["B"] = B
+    pol, rb = _make(S)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    rs = np.random.RandomState(B)
+    for step in (1, 2):
+        idx = rs.randint(0, gen.BUFFER_ROWS, B)
+        noise = rs.standard_normal((B, S["ad"])).astype(np.float32)
+        _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        out = pol.train_step(rb, B, indices=idx, noise=noise, stats=True)
+        assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5, (step, "y")
+        assert _rel_to_max(out["q1"], rec["q1"][:, 0]) <= 1e-5, (step, "q1")
+        assert _rel_to_max(out["q2"], rec["q2"][:, 0]) <= 1e-5, (step, "q2")
+        np.testing.assert_allclose(out["critic_loss"], rec["critic_loss"], rtol=1e-5)
+        if out["actor_step"]:
+            np.testing.assert_allclose(out["actor_loss"], rec["actor_loss"], rtol=1e-5, atol=1e-7)
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (step, "critic"))
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (step, "critic_target"))
