@@ -48,6 +48,8 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     r = subprocess.run(cmd, cwd=HERE, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
+    if "warning:" in r.stderr:                      # the build is expected to be warning-free
+        print(r.stderr[-6000:], file=sys.stderr)
     os.replace(tmp, OUT)
     return OUT
 

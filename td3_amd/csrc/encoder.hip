@@ -26,9 +26,10 @@ __device__ __forceinline__ float part_ld(const float* base, int n, int N, int D,
   return (n < N && d < D) ? gld(base + (size_t)n * D + d) : 0.f;
 }
 
-// v_writelane_b32: lane `lane` of `old` <- the uniform `val` (no builtin in this toolchain)
+// v_writelane_b32: lane `lane` of `old` <- the uniform `val` (no builtin in this toolchain).  The
+// lane select goes through M0 as a register-constrained operand, so the compiler owns M0.
 __device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t val, int lane) {
-  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "s"(lane) : "m0");
+  asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "{m0}"(lane));
   return old;
 }
 

@@ -111,7 +111,8 @@ struct DwProb {
   const float* GU; int ldgu;      // dU_l  (LN grads)
   const float* H; int ldh; const float* stats;
   int ntk;                        // k tiles of the weight
-  int tile_begin;                 // matrix tiles: (Np/32)*ntk, then vector tiles: Np/32
+  int tile_begin;                 // matrix tiles: (Np/T)*ntk (T = 32, or 64 with tile64), then
+                                  // vector tiles: Np/32
 };
 
 enum DwMode : int { kDwGrad = 0, kDwAdam = 1, kDwAdamPolyak = 2 };
@@ -129,6 +130,7 @@ struct DwArgs {
   DwProb probs[kMaxDwProbs]; int nprob; int Bp;
   AdamArgs adam;
   int mode;
+  int tile64;                     // 1: dw64_kernel (64x64 tiles, ntk counts k tiles of 64)
 };
 
 // ------------------------------------------------------------------ launchers (kernels.hip)

@@ -764,12 +764,49 @@ __global__ __launch_bounds__(256) void lnbwd_rows_kernel(const LnBwdProb* __rest
 }
 
 // ================================================================== Adam / Polyak (AdamK, adam_elem: dev.h)
-__device__ __forceinline__ void apply_grad(const DwArgs& a, const AdamK& k, int64_t idx, float g) {
+// N optimizer updates at once: every P/M/V(/T) load is issued before the first store, so the
+// element chain costs one memory round trip instead of N (the stores of one element could alias
+// the next element's loads for the compiler).
+template <int N>
+__device__ __forceinline__ void apply_grads(const DwArgs& a, const AdamK& k, const int64_t (&idx)[N],
+                                            const float (&g)[N], const bool (&ok)[N]) {
   if (a.mode == kDwGrad) {
-    gst(a.adam.G + (idx), g);
-  } else {
-    adam_elem(a.adam.P + idx, a.adam.M + idx, a.adam.V + idx, g, k,
-              a.mode == kDwAdamPolyak ? a.adam.T + idx : nullptr);
+#pragma unroll
+    for (int e = 0; e < N; ++e)
+      if (ok[e]) gst(a.adam.G + idx[e], g[e]);
+    return;
+  }
+  const bool pol = a.mode == kDwAdamPolyak;
+  int64_t any = -1;                                 // a valid index for the masked lanes' loads
+#pragma unroll
+  for (int e = N - 1; e >= 0; --e)
+    if (ok[e]) any = idx[e];
+  if (any < 0) return;
+  float mm[N], vv[N], pp[N], tt[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    const int64_t j = ok[e] ? idx[e] : any;
+    mm[e] = gld(a.adam.M + j);
+    vv[e] = gld(a.adam.V + j);
+    pp[e] = gld(a.adam.P + j);
+    tt[e] = pol ? gld(a.adam.T + j) : 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e) {                    // torch _single_tensor_adam, as adam_elem
+    mm[e] = __fmaf_rn(k.w1, g[e] - mm[e], mm[e]);
+    vv[e] = vv[e] * k.b2;
+    vv[e] = vv[e] + (k.c2 * g[e]) * g[e];
+    const float denom = sqrtf(vv[e]) / k.bc2s + k.eps;
+    pp[e] = pp[e] + (k.negss * mm[e]) / denom;
+    tt[e] = k.tau * pp[e] + k.omt * tt[e];
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    if (!ok[e]) continue;
+    gst(a.adam.M + idx[e], mm[e]);
+    gst(a.adam.V + idx[e], vv[e]);
+    gst(a.adam.P + idx[e], pp[e]);
+    if (pol) gst(a.adam.T + idx[e], tt[e]);
   }
 }
 
@@ -782,6 +819,62 @@ __device__ __forceinline__ void dw_load_chunk(const DwProb& P, int rc, int h, in
   for (int s = 0; s < 16; ++s) {
     av[s] = gld(gp + (size_t)s * P.ldg);
     bv[s] = gld(up + (size_t)s * P.ldu);
+  }
+}
+
+// Vector tile j of a problem: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU over 32 columns
+// (NT/32 row groups of 8-row strides), then the optimizer update of those 32 columns.
+template <int NT>
+__device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P, const AdamK& k, int j,
+                                               float* red) {
+  constexpr int NG = NT / 32;
+  const int n0 = j * 32;
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const bool ln = P.offg >= 0;
+  const bool hasb = P.offb >= 0;                    // false: a LayerNorm-only problem (lnorm1)
+  float sb = 0.f, sg = 0.f, sbeta = 0.f;
+  for (int r0 = rg; r0 < a.Bp; r0 += 8 * NG) {
+    float gz[8], gu[8], hh[8], mu[8], rs[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = min(r0 + NG * u, a.Bp - 1);     // clamped: loads stay unconditional
+      gz[u] = hasb ? gld(P.G + ((size_t)r * P.ldg + n0 + c)) : 0.f;
+      if (ln) {
+        gu[u] = gld(P.GU + ((size_t)r * P.ldgu + n0 + c));
+        hh[u] = gld(P.H + ((size_t)r * P.ldh + n0 + c));
+        mu[u] = gld(P.stats + r);
+        rs[u] = gld(P.stats + (a.Bp + r));
+      }
+      if (r0 + NG * u >= a.Bp) {
+        gz[u] = 0.f;
+        gu[u] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      sb += gz[u];
+      if (ln) {
+        sg += gu[u] * ((hh[u] - mu[u]) * rs[u]);
+        sbeta += gu[u];
+      }
+    }
+  }
+  red[(0 * NG + rg) * 32 + c] = sb;
+  red[(1 * NG + rg) * 32 + c] = sg;
+  red[(2 * NG + rg) * 32 + c] = sbeta;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      s0 += red[(0 * NG + g) * 32 + c];
+      s1 += red[(1 * NG + g) * 32 + c];
+      s2 += red[(2 * NG + g) * 32 + c];
+    }
+    const int64_t idx[3] = {P.offb + n0 + c, P.offg + n0 + c, P.offbeta + n0 + c};
+    const float gq[3] = {s0, s1, s2};
+    const bool ok[3] = {hasb, ln, ln};
+    apply_grads<3>(a, k, idx, gq, ok);
   }
 }
 
@@ -825,6 +918,9 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
     __syncthreads();
+    int64_t idx[4];
+    float gq[4];
+    bool ok[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = threadIdx.x + 256 * q;
@@ -832,59 +928,112 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
       float g = red[n * 33 + kk];
 #pragma unroll
       for (int w = 1; w < 4; ++w) g = g + red[(w * 32 + n) * 33 + kk];
-      apply_grad(a, k, P.offW + (int64_t)(n0 + n) * P.Kp + k0 + kk, g);
+      idx[q] = P.offW + (int64_t)(n0 + n) * P.Kp + k0 + kk;
+      gq[q] = g;
+      ok[q] = true;
     }
+    apply_grads<4>(a, k, idx, gq, ok);
     return;
   }
-  // ---- vector tile
-  const int n0 = (t - nmat) * 32;
-  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const bool ln = P.offg >= 0;
-  const bool hasb = P.offb >= 0;                    // false: a LayerNorm-only problem (lnorm1)
-  float sb = 0.f, sg = 0.f, sbeta = 0.f;
-  for (int r0 = rg; r0 < a.Bp; r0 += 64) {
-    float gz[8], gu[8], hh[8], mu[8], rs[8];
+  dw_vector_tile<256>(a, P, k, t - nmat, red);
+}
+
+// Large batches (Bp >= 512): 64x64 weight tiles per workgroup of 8 waves.  Each step stages 64
+// rows of dZ[:, n0:n0+64] and U[:, k0:k0+64] in LDS (one float4 per thread and operand, the next
+// 64 rows in flight in registers); wave w multiplies quadrant (w&3) over the 32-row half w>>2.
+// Per 32x32 output this reads half the operand bytes of dw_kernel's register tiles, the bound
+// at B >= 512.  The two row halves meet in LDS; the rh=0 waves apply the optimizer update.
+constexpr int kDw64S = 66;                          // LDS row stride: rows 16 apart 32 banks apart
+constexpr int kDw64Depth = 2;                       // 64-row steps in flight (1, 3, 5: no change)
+__global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
+  __shared__ float sm[2 * 2 * 64 * kDw64S];         // [buf][operand][64 rows][kDw64S]
+  const int b = xcd_tile(nb);
+  if (b >= nb) return;
+  int pi = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = min(r0 + 8 * u, a.Bp - 1);      // clamped: loads stay unconditional
-      gz[u] = hasb ? gld(P.G + ((size_t)r * P.ldg + n0 + c)) : 0.f;
-      if (ln) {
-        gu[u] = gld(P.GU + ((size_t)r * P.ldgu + n0 + c));
-        hh[u] = gld(P.H + ((size_t)r * P.ldh + n0 + c));
-        mu[u] = gld(P.stats + r);
-        rs[u] = gld(P.stats + (a.Bp + r));
-      }
-      if (r0 + 8 * u >= a.Bp) {
-        gz[u] = 0.f;
-        gu[u] = 0.f;
-      }
+  for (int i = 1; i < kMaxDwProbs; ++i)
+    if (i < a.nprob && b >= a.probs[i].tile_begin) pi = i;
+  const DwProb& P = a.probs[pi];
+  const int t = b - P.tile_begin;
+  const int ntn = (P.Np + 63) >> 6;
+  const int nmat = ntn * P.ntk;                      // ntk = k tiles of 64 in this mode
+  const AdamK k = make_adam(a.adam);
+  if (t >= nmat) {
+    dw_vector_tile<512>(a, P, k, t - nmat, sm);
+    return;
+  }
+  const int kt = t % P.ntk, nt = t / P.ntk;
+  const int n0 = nt * 64, k0 = kt * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
+  // staging: float4 e = tid and tid + 512 of each operand's 64x64 block: row e>>4, cols 4(e&15);
+  // kDw64Depth steps of 64 rows are in flight in registers (HBM latency > one step's 16 MFMAs)
+  constexpr int D = kDw64Depth;
+  float4 sg[D][2], su[D][2];
+  auto fetch = [&](int r0, float4 (&g)[2], float4 (&u)[2]) {
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int e = tid + 512 * v, row = r0 + (e >> 4), c4 = (e & 15) * 4;
+      const bool live = row < a.Bp;
+      g[v] = (live && n0 + c4 < P.Np) ? gld4(P.G + (size_t)row * P.ldg + n0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      u[v] = (live && k0 + c4 < P.Kp) ? gld4(P.U + (size_t)row * P.ldu + k0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  };
+  auto put = [&](int buf, const float4 (&gq)[2], const float4 (&uq)[2]) {
+    float* g = sm + buf * 2 * 64 * kDw64S;
+    float* uu = g + 64 * kDw64S;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      sb += gz[u];
-      if (ln) {
-        sg += gu[u] * ((hh[u] - mu[u]) * rs[u]);
-        sbeta += gu[u];
-      }
+    for (int v = 0; v < 2; ++v) {
+      const int e = tid + 512 * v, row = e >> 4, c4 = (e & 15) * 4;
+      float* gp = g + row * kDw64S + c4;
+      float* up = uu + row * kDw64S + c4;
+      gp[0] = gq[v].x; gp[1] = gq[v].y; gp[2] = gq[v].z; gp[3] = gq[v].w;
+      up[0] = uq[v].x; up[1] = uq[v].y; up[2] = uq[v].z; up[3] = uq[v].w;
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int nstep = (a.Bp + 63) >> 6;
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < nstep) fetch(d * 64, sg[d], su[d]);
+  for (int st0 = 0; st0 < nstep; st0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int st = st0 + d;
+      if (st >= nstep) break;
+      const int buf = st & 1;
+      put(buf, sg[d], su[d]);
+      __syncthreads();
+      if (st + D < nstep) fetch((st + D) * 64, sg[d], su[d]);
+      const float* g = sm + buf * 2 * 64 * kDw64S + (rh * 32 + 16 * h) * kDw64S;
+      const float* uu = g + 64 * kDw64S;
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2)
+        acc = mfma32x32x2(g[s2 * kDw64S + qn * 32 + i], uu[s2 * kDw64S + qk * 32 + i], acc);
     }
   }
-  red[(0 * 8 + rg) * 32 + c] = sb;
-  red[(1 * 8 + rg) * 32 + c] = sg;
-  red[(2 * 8 + rg) * 32 + c] = sbeta;
-  __syncthreads();
-  if (threadIdx.x < 32) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  __syncthreads();                                   // staging buffers become the reduction tile
+  float* red = sm + (wave & 3) * 32 * 33;
+  if (rh == 1) {
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      s0 += red[(0 * 8 + g) * 32 + c];
-      s1 += red[(1 * 8 + g) * 32 + c];
-      s2 += red[(2 * 8 + g) * 32 + c];
+    for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[r];
+  }
+  __syncthreads();
+  if (rh == 0) {
+    const int kk = k0 + qk * 32 + i;
+    int64_t idx[16];
+    float gq[16];
+    bool ok[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + qn * 32 + mfma_row(r, lane);
+      gq[r] = acc[r] + red[mfma_row(r, lane) * 33 + i];
+      ok[r] = n < P.Np && kk < P.Kp;
+      idx[r] = P.offW + (int64_t)n * P.Kp + kk;
     }
-    if (hasb) apply_grad(a, k, P.offb + n0 + c, s0);
-    if (ln) {
-      apply_grad(a, k, P.offg + n0 + c, s1);
-      apply_grad(a, k, P.offbeta + n0 + c, s2);
-    }
+    apply_grads<16>(a, k, idx, gq, ok);
   }
 }
 
@@ -988,7 +1137,10 @@ int launch_lnbwd_rows(const LnBwdProb* d, int nprob, int Bp, int norm, hipStream
 
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s) {
   if (nblocks <= 0) return 0;
-  hipLaunchKernelGGL(dw_kernel, dim3((nblocks + 7) & ~7), dim3(256), 0, s, a, nblocks);
+  if (a.tile64)
+    hipLaunchKernelGGL(dw64_kernel, dim3((nblocks + 7) & ~7), dim3(512), 0, s, a, nblocks);
+  else
+    hipLaunchKernelGGL(dw_kernel, dim3((nblocks + 7) & ~7), dim3(256), 0, s, a, nblocks);
   TD3_HIP(hipGetLastError());
   return 0;
 }

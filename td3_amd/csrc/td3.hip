@@ -493,6 +493,10 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                         Group& g, int which, const std::vector<BwdItem>& items, int Bp,
                         const char* tag, bool polyak, int enc_nwg = 0) {
   const bool norm = h->cfg.norm != 0;
+  // B >= 512: 64x64 weight tiles with LDS-staged operands (dw64_kernel: half the operand
+  // traffic, Humanoid C_dw 73 -> 63 us), else 32x32 register tiles (dw_kernel: more, shorter
+  // workgroups for the latency-bound small batches)
+  const bool tile64 = Bp >= 512;
   std::vector<DwProb> probs;
   int blocks = 0;
   double flops = 0;
@@ -521,9 +525,9 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
         p.offg = -1;
         p.offbeta = -1;
       }
-      p.ntk = L.Kp / 32;
+      p.ntk = tile64 ? (L.Kp + 63) / 64 : L.Kp / 32;
       p.tile_begin = blocks;
-      blocks += (L.Np / 32) * p.ntk + L.Np / 32;     // matrix tiles, then vector tiles
+      blocks += (tile64 ? (L.Np + 63) / 64 : L.Np / 32) * p.ntk + L.Np / 32;   // matrix, then vector tiles
       flops += 2.0 * Bp * L.N * L.K;
       probs.push_back(p);
     }
@@ -564,8 +568,9 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.adam.grad_scale = 1.0f;
   const bool dp = h->comm != nullptr;
   a.mode = dp ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
+  a.tile64 = tile64 ? 1 : 0;
   st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
-                "td3::dw_kernel"});
+                tile64 ? "td3::dw64_kernel" : "td3::dw_kernel"});
   if (enc_nwg > 0) {
     EncAdamArgs ea{};
     for (auto& it : items) {

@@ -18,7 +18,7 @@ for k in range(1, n + 1):
             name = re.sub(r"\(.*$", "", r["Kernel_Name"]).replace("void ", "").strip()
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for name, d in sorted(acc.items()):
-    if not any(x in name for x in ("enc_", "gemm", "dw_", "row_")):
+    if not any(x in name for x in ("enc_", "gemm", "dw", "row_")):
         continue
     print(name, {c: round(sum(v) / len(v), 1) for c, v in sorted(d.items())})
 PY
