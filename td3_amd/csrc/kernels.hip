@@ -1082,8 +1082,10 @@ static GemmFn pick_bwd(int pro) {
 
 static GemmFn pick_gemm(int mode, int wn, int pro) {
   if (mode == 0 && wn == 1) return pick_fwd<1>(pro);
+  if (mode == 0 && wn == 2) return pick_fwd<2>(pro);
   if (mode == 0 && wn == 4) return pick_fwd<4>(pro);
   if (mode == 1 && wn == 1) return pick_bwd<1>(pro);
+  if (mode == 1 && wn == 2) return pick_bwd<2>(pro);
   if (mode == 1 && wn == 4) return pick_bwd<4>(pro);
   return nullptr;
 }
@@ -1176,6 +1178,7 @@ static int set_attr_all() {
 
 int kernels_init() {
   int rc = set_attr_all<1>();
+  if (!rc) rc = set_attr_all<2>();
   if (!rc) rc = set_attr_all<4>();
   return rc;
 }

@@ -320,14 +320,18 @@ static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<
   return 0;
 }
 
-// Output columns per GEMM workgroup.  32 (WN=1, K split 8 ways) gives the shortest MFMA chain:
-// right for the latency-bound B=256 stages (WN=4 there measured slower: HalfCheetah F_fwd1
-// 14.8 -> 18.3 us).  At B >= 512 a stage of >= 256 such workgroups is bound by the A rows and
-// weights every 32-column tile re-reads; 128 columns per workgroup (WN=4, K split 2 ways, wide K
-// streamed chunk by chunk) cut that traffic: Humanoid B=1024 2.70k -> 2.92k steps/s, particles
-// B=4096 MLP stages -20 %.  Narrow K (<= 128) always uses WN=4.
-static int gemm_wn(int maxK, int Bp, int wn1_blocks) {
-  return (maxK <= 128 || (Bp >= 512 && wn1_blocks >= 256)) ? 4 : 1;
+// Output columns per GEMM workgroup.  32 (WN=1, K split 8 ways) gives the shortest MFMA chain,
+// right for most latency-bound B=256 stages.  A stage of >= 256 such workgroups is bound by the
+// A rows and weights that every 32-column tile re-reads instead:
+//   * B >= 512: 128 columns (WN=4, K split 2 ways, wide K streamed chunk by chunk): Humanoid
+//     B=1024 2.70k -> 2.92k steps/s, particles B=4096 MLP stages -20 %;
+//   * B = 256 forward stages (3-4 networks): 64 columns (WN=2): HalfCheetah F_fwd1 15.0 ->
+//     13.8 us, F_fwd2 13.9 -> 12.4 us; WN=4 there is slower (18.3 us), and the input-grad
+//     stages (strided weight reads) lose with WN=2 (CB_bwd1 9.0 -> 10.8 us).
+// Narrow K (<= 128) always uses WN=4.
+static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd) {
+  if (maxK <= 128 || (Bp >= 512 && wn1_blocks >= 256)) return 4;
+  return (fwd && wn1_blocks >= 256) ? 2 : 1;
 }
 
 // Forward layers 0..2 of several networks (one launch per layer); layer 0 copies the
@@ -344,7 +348,7 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       maxKp = std::max(maxKp, it.net->lin[l].Kp);
       wn1_blocks += (Bp / 32) * ((it.net->lin[l].Np + 31) / 32);
     }
-    const int wn = gemm_wn(maxKp, Bp, wn1_blocks);
+    const int wn = gemm_wn(maxKp, Bp, wn1_blocks, true);
     const bool lnin = items[0].net->lnin;          // TD3_particles lnorm1 on the MLP input
     const int pro = l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
     int blocks = 0, lds = 0;
@@ -421,7 +425,7 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       maxKp = std::max(maxKp, it.net->lin[l].Np);
       wn1_blocks += (Bp / 32) * ((it.net->lin[l].Kp + 31) / 32);
     }
-    const int wn = gemm_wn(maxKp, Bp, wn1_blocks);
+    const int wn = gemm_wn(maxKp, Bp, wn1_blocks, false);
     for (size_t k = 0; k < items.size(); ++k) {
       const BwdItem& it = items[k];
       const LinearL& L = it.net->lin[l];
