@@ -164,9 +164,15 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="halfcheetah")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--eager", action="store_true", help="disable hipGraph replay")
+    ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
+                    help="step launch mode: hipGraph replay, direct launches, or auto (replay while the "
+                         "GPU has caught up with the host, direct launches while steps are queued)")
+    ap.add_argument("--eager", action="store_true", help="same as --launch eager")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.eager:
+        args.launch = "eager"
+    use_graph = {"auto": "auto", "graph": True, "eager": False}[args.launch]
     B, REPLAY_ROWS = cfg["batch"], cfg["replay"]
 
     import torch
@@ -187,13 +193,13 @@ def main():
         from td3_amd.my_replay_buffer import ReplayBuffer_particles as RB
         obs = (Box((cfg["F"],)), Box((cfg["N"], cfg["D"])))
         pol = TD3(obs, Box((cfg["ad"],)), norm="layer", device=local, seed=17 + rank,
-                  use_graph=not args.eager)
+                  use_graph=use_graph)
     else:
         from td3_amd.TD3_featured import TD3
         from td3_amd.my_replay_buffer import ReplayBuffer_featured as RB
         obs = Box((cfg["sd"],))
         pol = TD3(obs, Box((cfg["ad"],)), max_action=cfg["ma"], norm="layer", device=local,
-                  seed=17 + rank, use_graph=not args.eager)
+                  seed=17 + rank, use_graph=use_graph)
     rb = RB(obs, Box((cfg["ad"],)), max_size=REPLAY_ROWS, device=local, seed=101 + rank)
     rb.fill_synthetic(REPLAY_ROWS, cfg["ma"], seed=7 + rank)
     if world > 1:
@@ -269,7 +275,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "replay_per_gpu": REPLAY_ROWS,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "global_steps_per_s": round(gsteps, 3),
-                       "graph": not args.eager},
+                       "launch": args.launch},
         }
         if roof is not None:
             out["roofline"] = roof

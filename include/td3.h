@@ -104,7 +104,9 @@ typedef struct td3_config {
   double lr, beta1, beta2, eps;                     /* torch.optim.Adam defaults */
   uint64_t seed;           /* Philox key for index draws and target-policy noise */
   int device;
-  int use_graph;           /* capture each step variant into a hipGraph (default 1) */
+  int use_graph;           /* 0: direct launches; 1: replay each step variant as a hipGraph;
+                              2 (default): graph replay while the GPU has caught up with the host,
+                              direct launches while earlier steps are still queued */
   /* TD3_particles (TD3_particles.py): state = (features [F], particles [N][D]); the Q head has
    * action_dim outputs; state_dim = F, hidden widths (500, 400, 300) for actor and critic. */
   int particles;           /* 0: TD3_featured, 1: TD3_particles */

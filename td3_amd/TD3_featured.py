@@ -184,7 +184,7 @@ class TD3(TD3_base):
     """TD3_featured.TD3 (TD3_featured.py:99-171) on the HIP pipeline."""
 
     def __init__(self, obs_space, action_space, max_action=1, lr=1e-4, norm=None, CDQ=True,
-                 device=None, seed=0, use_graph=True, actor_arch=ACTOR_ARCH, q_arch=Q_ARCH,
+                 device=None, seed=0, use_graph="auto", actor_arch=ACTOR_ARCH, q_arch=Q_ARCH,
                  init="torch", **kwargs):
         super().__init__(max_action=max_action, **kwargs)
         self._lib = _lib.load()
@@ -212,7 +212,7 @@ class TD3(TD3_base):
         cfg.lr = float(lr)
         cfg.seed = int(seed)
         cfg.device = self._dev
-        cfg.use_graph = 1 if use_graph else 0
+        cfg.use_graph = 2 if use_graph == "auto" else (1 if use_graph else 0)
         self._cfg = cfg
         h = C.c_void_p()
         check(self._lib.td3_create(C.byref(cfg), C.byref(h)), "td3_create")

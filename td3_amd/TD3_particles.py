@@ -81,7 +81,7 @@ class TD3(_FeaturedTD3):
     """TD3_particles.TD3 (TD3_particles.py:135-224) on the HIP pipeline."""
 
     def __init__(self, obs_space, action_space, lr=1e-4, norm=None, CDQ=True, device=None, seed=0,
-                 use_graph=True, init="torch", **kwargs):
+                 use_graph="auto", init="torch", **kwargs):
         TD3_base.__init__(self, **kwargs)
         self._lib = _lib.load()
         if norm not in (None, "layer"):
@@ -110,7 +110,7 @@ class TD3(_FeaturedTD3):
         cfg.lr = float(lr)
         cfg.seed = int(seed)
         cfg.device = self._dev
-        cfg.use_graph = 1 if use_graph else 0
+        cfg.use_graph = 2 if use_graph == "auto" else (1 if use_graph else 0)
         cfg.particles = 1
         cfg.n_particles, cfg.particle_dim = N, D
         cfg.cdq = 1 if self.CDQ else 0

@@ -23,6 +23,8 @@ enum Pro : int {
   kProCopy = 0,        // A rows as stored (network inputs, dZ rows from a row kernel)
   kProLN = 1,          // LayerNorm of the previous hidden layer (ReLU -> LN order)
   kProLNBwd = 2,       // dZ = relu'(LN_bwd(dU)) of the following layer
+  kProGather = 3,      // replay-ring rows of this step: Philox index draw + record read (the
+                       // sample() of my_replay_buffer.py:119-128 fused into the first layer)
 };
 
 // Row kernels (one batch row per wave) between the GEMM stages; they reuse GemmProb's
@@ -63,12 +65,24 @@ struct GemmProb {
   const Counters* ctr;
 };
 
+// kProGather: the step's replay-ring sample.  Every workgroup draws the indices of its 32 rows
+// (Philox step = total_it + 1, exactly as gather_kernel) and reads its A rows from the records
+// (GemmProb::exi[0] = offset of the row inside the record, Kreal = its width).
+struct RingSide {
+  const float* data; int rec;
+  const int64_t* d_size;          // sample range [0, *d_size)
+  int64_t* idx_out;               // drawn rows (td3_step_stats.idx)
+  uint64_t seed;
+  const Counters* ctr;
+};
+
 // Problems of one GEMM / row launch, passed BY VALUE in the kernel arguments (one scalar
 // load level fewer than a device table at the head of every workgroup's dependency chain).
 constexpr int kMaxProbs = 4;
 struct GemmTable {
   GemmProb p[kMaxProbs];
   int nprob;
+  RingSide rs;                    // kProGather only
 };
 
 // ------------------------------------------------------------------ row-wise heads (act / eval_q)

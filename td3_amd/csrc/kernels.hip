@@ -103,6 +103,64 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
   }
 }
 
+// Replay-ring rows (kProGather): the step's sample (my_replay_buffer.py:119-128) drawn and read
+// by the first layer itself.  Row indices: Philox(seed, total_it + 1, row) over [0, size), the
+// same draw as gather_kernel; padded rows (>= B) are zero.  Record fields are not 16-B aligned,
+// so the lane slices are dword loads.
+__device__ __forceinline__ void rv_load_u(float (&v)[8], const float* __restrict__ p, int len, int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = rcol(lane, j);
+    v[j] = col < len ? gld(p + col) : 0.f;
+  }
+}
+
+// A problem's first column tile also stores its rows for the later stages (no extra loads):
+// Aout (+ ex[0], ld exi[3]) = the A row; ex[1] / ex[2] = reward / not_done (record offset
+// exi[1], exi[1] + 1); problem 0 records the drawn rows.
+__device__ __forceinline__ void pro_gather(const GemmProb& P, const RingSide& rs, float* smem, const Ctx& c,
+                                           int pi) {
+  const uint64_t step = (uint64_t)(rs.ctr->total_it + 1);
+  const uint64_t n = (uint64_t)*rs.d_size;
+  int64_t idx[kRPW];
+#pragma unroll
+  for (int r = 0; r < kRPW; ++r) {
+    const int grow = c.m0 + c.wave * kRPW + r;
+    idx[r] = grow < P.B ? (int64_t)philox_index(rs.seed, step, (uint32_t)grow, n) : -1;
+  }
+  const bool t0 = c.nt == 0;
+  float x[kRPW][8], rw[kRPW];
+#pragma unroll
+  for (int r = 0; r < kRPW; ++r) {
+    rw[r] = 0.f;
+    if (idx[r] >= 0) {
+      const float* rec = rs.data + (size_t)idx[r] * rs.rec;
+      rv_load_u(x[r], rec + P.exi[0], P.Kreal, c.lane);
+      if (t0 && c.lane < 2 && P.ex[1 + c.lane]) rw[r] = gld(rec + P.exi[1] + c.lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[r][j] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kRPW; ++r) lds_put_row(smem, c.S, c.wave * kRPW + r, P.Kp, c.lane, x[r]);
+  if (!t0) return;
+#pragma unroll
+  for (int r = 0; r < kRPW; ++r) {
+    const int grow = c.m0 + c.wave * kRPW + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = rcol(c.lane, j);
+      if (col < P.Kreal) {
+        if (P.Aout) gst(P.Aout + (size_t)grow * P.ldao + col, x[r][j]);
+        if (P.ex[0]) gst(P.ex[0] + (size_t)grow * P.exi[3] + col, x[r][j]);
+      }
+    }
+    if (c.lane < 2 && P.ex[1 + c.lane]) gst(P.ex[1 + c.lane] + grow, rw[r]);
+    if (pi == 0 && rs.idx_out && c.lane == 0 && grow < P.B) rs.idx_out[grow] = idx[r];
+  }
+}
+
 // ================================================================== row kernels
 // One batch row per wave (grid: Bp/4 x nprob, 256 threads): the head / loss work between the
 // GEMM stages.  Every operand of the row (and the head weights) is requested up front, the
@@ -629,6 +687,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   if constexpr (PRO == kProCopy) pro_copy<kRPW>(P, smem, c);
   else if constexpr (PRO == kProLN) pro_ln(P, smem, c);
   else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
+  else if constexpr (PRO == kProGather) pro_gather(P, tab.rs, smem, c, pi);
   __syncthreads();
 
   f32x16 acc;
@@ -1067,6 +1126,7 @@ static GemmFn pick_fwd(int pro) {
   switch (pro) {
     case kProCopy: return gl<0, WN, kProCopy>;
     case kProLN: return gl<0, WN, kProLN>;
+    case kProGather: return gl<0, WN, kProGather>;
   }
   return nullptr;
 }
@@ -1170,6 +1230,7 @@ static int set_attr_all() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, max_lds))
   TD3_ATTR(0, kProCopy);
   TD3_ATTR(0, kProLN);
+  TD3_ATTR(0, kProGather);
   TD3_ATTR(1, kProCopy);
   TD3_ATTR(1, kProLNBwd);
 #undef TD3_ATTR

@@ -182,6 +182,9 @@ struct Plan {
   std::vector<void*> tables;
   // stage lists (excluding the input stage): [actor_phase][inject_noise]
   std::vector<Stage> body[2][2];
+  // featured replay-ring bodies: the sample fused into F_fwd0 (kProGather), ring bound in rside
+  std::vector<Stage> body_ring[2][2];
+  RingSide rside{};
   hipGraphExec_t graph[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   // the same bodies with the replay-ring gather captured in front (Philox draw path)
   hipGraphExec_t graph_g[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -285,13 +288,23 @@ static int gemm_lds_bytes(int Kp) {
 
 // store_u: keep the LN outputs U (input of the dW of the next layer);
 // stats: keep the LN row statistics (needed by any backward through this network).
-struct FwdItem { const NetL* net; const float* P; EvalB* e; bool store_u; bool stats; };
+// Batch buffers the ring-sampled first layer fills (first column tile of a problem).
+struct RingOut {
+  float* a; int lda;      // the A row
+  float* b; int ldb;      // a second copy of it
+  float* r; float* nd;    // reward, not_done
+};
+
+struct FwdItem {
+  const NetL* net; const float* P; EvalB* e; bool store_u; bool stats;
+  int ring_src = -1;      // layer 0 read from the replay ring (kProGather): record offset of the input
+};
 struct BwdItem { const NetL* net; const float* P; EvalB* e; bool store_dz; };
 
 static int push_gemm_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                            std::vector<GemmProb>& probs, int mode, int wn, int pro, int Bp, int lds,
                            int blocks, double flops, const std::string& name, Counters* bump,
-                           int bump_actor) {
+                           int bump_actor, const RingSide* rs = nullptr) {
   (void)h;
   (void)owned;
   TD3_ARG(!probs.empty() && probs.size() <= (size_t)kMaxProbs, "too many problems in one gemm stage");
@@ -300,6 +313,20 @@ static int push_gemm_stage(td3_handle* h, std::vector<void*>& owned, std::vector
   t.nprob = (int)probs.size();
   char kname[64];
   snprintf(kname, sizeof(kname), "td3::gemm_kernel<%d, %d, %d>", mode, wn, pro);
+  if (rs) {      // the ring bound at launch (capture) time: Plan::rside, filled by bind_ring
+    st.push_back({name,
+                  [=](hipStream_t s) {
+                    GemmTable tt = t;
+                    tt.rs = *rs;
+                    if (!tt.rs.data) {
+                      set_error("internal: ring-sampled stage launched without a bound ring");
+                      return -1;
+                    }
+                    return launch_gemm(mode, wn, pro, tt, blocks, Bp, lds, bump, bump_actor, s);
+                  },
+                  flops, kname});
+    return 0;
+  }
   st.push_back({name,
                 [=](hipStream_t s) { return launch_gemm(mode, wn, pro, t, blocks, Bp, lds, bump, bump_actor, s); },
                 flops, kname});
@@ -338,7 +365,8 @@ static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd) {
 // network input rows, layers 1 and 2 apply the previous layer's LayerNorm in the prologue.
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
-                          Counters* bump, int bump_actor) {
+                          Counters* bump, int bump_actor, const RingSide* ring = nullptr,
+                          const RingOut* ro = nullptr, int o_r = 0) {
   const bool norm = h->cfg.norm != 0;
   for (int l = 0; l < 3; ++l) {
     std::vector<GemmProb> probs;
@@ -350,7 +378,8 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     }
     const int wn = gemm_wn(maxKp, Bp, wn1_blocks, true);
     const bool lnin = items[0].net->lnin;          // TD3_particles lnorm1 on the MLP input
-    const int pro = l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
+    const bool gather = ring && l == 0;
+    const int pro = gather ? kProGather : l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
     int blocks = 0, lds = 0;
     double flops = 0;
     for (size_t k = 0; k < items.size(); ++k) {
@@ -384,6 +413,17 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
           }
         }
       }
+      if (gather) {
+        TD3_ARG(it.ring_src >= 0 && !lnin && ro, "internal: ring-sampled layer without a record field");
+        p.exi[0] = it.ring_src;
+        p.Aout = ro[k].a;
+        p.ldao = ro[k].lda;
+        p.ex[0] = ro[k].b;
+        p.exi[3] = ro[k].ldb;
+        p.ex[1] = ro[k].r;
+        p.ex[2] = ro[k].nd;
+        p.exi[1] = o_r;
+      }
       p.Kreal = L.K;
       p.Kp = L.Kp;
       p.W = it.P + L.offW;
@@ -401,8 +441,8 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       probs.push_back(p);
     }
     TD3_RC(push_gemm_stage(h, owned, st, probs, 0, wn, pro, Bp, lds, blocks, flops,
-                           std::string(tag) + "_fwd" + std::to_string(l), l == 0 ? bump : nullptr,
-                           bump_actor));
+                           std::string(tag) + "_fwd" + std::to_string(l), l == 1 ? bump : nullptr,
+                           bump_actor, gather ? ring : nullptr));
   }
   return 0;
 }
@@ -742,6 +782,24 @@ static int build_step(td3_handle* h, int B) {
                                  {&q2, Pq2, &P->Q[1], true, true}};
       if (actor_phase) f1.push_back({&an, Pa, &P->A, true, true});
       TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase));
+      {  // the ring-sampled first layer (record layout [s | a | s' | r | not_done], replay.hip)
+        // the first column tile of each problem keeps what the later stages read: the target-twin
+        // input s' (X_S2A), the twin dW input [s | a] (X_SA), reward / not_done, and on policy
+        // steps the actor dW input s (X_S) and the policy-Q input s (X_SP)
+        std::vector<FwdItem> f1r = f1;
+        f1r[0].ring_src = sd + ad;                   // target actor on s'
+        f1r[1].ring_src = 0;                         // twin on [s | a]
+        f1r[2].ring_src = 0;
+        if (actor_phase) f1r[3].ring_src = 0;        // actor on s
+        std::vector<Stage> fr;
+        RingOut ro[4] = {{P->X_S2A, P->ld_sa, nullptr, 0, nullptr, nullptr},
+                         {P->X_SA, P->ld_sa, nullptr, 0, nullptr, nullptr},
+                         {nullptr, 0, nullptr, 0, P->R, P->ND},
+                         {P->X_S, P->ld_s, P->X_SP, P->ld_sa, nullptr, nullptr}};
+        TD3_RC(add_fwd_stages(h, P->tables, fr, f1r, Bp, B, "F", h->d_ctr, actor_phase, &P->rside, ro,
+                              2 * sd + ad));
+        P->body_ring[actor_phase][inj].push_back(fr[0]);
+      }
       // ---- heads: a' = target smoothing into X_S2A (:131-137); pi(s) into X_SP (:159)
       {
         std::vector<GemmProb> hp = {policy_head(Pta, P->TA, P->X_S2A, 1, inj ? 0 : 1)};
@@ -856,6 +914,11 @@ static int build_step(td3_handle* h, int B) {
       TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true));
     }
   }
+  for (int a = 0; a < 2; ++a)          // ring bodies: F_fwd0 sampled from the ring, the rest shared
+    for (int i = 0; i < 2; ++i) {
+      std::vector<Stage>& br = P->body_ring[a][i];
+      br.insert(br.end(), P->body[a][i].begin() + 1, P->body[a][i].end());
+    }
   if (h->plan) destroy_plan(h->plan.get());
   h->plan = std::move(P);
   return 0;
@@ -1323,10 +1386,17 @@ static int input_from_batch(td3_handle* h, Plan* P, const float* s, const float*
 // launched first and, in graph mode, captured into the same hipGraph (one replay per step).
 static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring* ring) {
   Plan* P = h->plan.get();
-  std::vector<Stage>& st = P->body[actor_phase][inj];
+  const bool fused = ring && !P->particles;      // featured: the sample runs inside F_fwd0
+  std::vector<Stage>& st = fused ? P->body_ring[actor_phase][inj] : P->body[actor_phase][inj];
   h->last_body = &st;
-  if (!h->cfg.use_graph) {
-    if (ring) TD3_RC(input_from_ring(h, ring, P, false, s));
+  // use_graph 2 (auto): a hipGraph replay costs ~8 us of GPU time on top of its kernels
+  // (tools/launch_floor.hip) but little host time; direct launches cost the host ~3 us each and
+  // the GPU nothing extra.  While the last policy step is still queued the host is ahead of the
+  // GPU, so its launch time is hidden: launch directly.  Otherwise (host-bound loops) replay.
+  const bool graph = h->cfg.use_graph == 1 ||
+                     (h->cfg.use_graph == 2 && hipEventQuery(h->actor_ev) != hipErrorNotReady);
+  if (!graph) {
+    if (ring && !fused) TD3_RC(input_from_ring(h, ring, P, false, s));
     return run_stages(st, s);
   }
   if (ring && P->graph_ring != ring) {          // graphs bake the ring's pointers in
@@ -1343,7 +1413,7 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
     hipStream_t cs;
     TD3_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     TD3_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    int rc = ring ? input_from_ring(h, ring, P, false, cs) : 0;
+    int rc = ring && !fused ? input_from_ring(h, ring, P, false, cs) : 0;
     if (!rc) rc = run_stages(st, cs);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(cs, &g);
@@ -1374,9 +1444,26 @@ static int ensure_plan(td3_handle* h, int B) {
 }
 
 // A particle learner's encoders read the ring the step samples from.
-static void bind_ring(td3_handle* h, Ring* r) {
+// A featured learner's first layer samples the ring (kProGather; record layout checked at plan
+// build against replay.hip's [s | a | s' | r | not_done]).
+static int bind_ring(td3_handle* h, Ring* r) {
   Plan* P = h->plan.get();
-  if (P->particles) set_particle_source(P, r, r->data, r->rec, r->o_p, r->o_p2, P->d_idx);
+  if (P->particles) {
+    set_particle_source(P, r, r->data, r->rec, r->o_p, r->o_p2, P->d_idx);
+    return 0;
+  }
+  const int sd = h->sd, ad = h->ad;
+  TD3_ARG(r->o_s == 0 && r->o_a == sd && r->o_s2 == sd + ad && r->o_r == 2 * sd + ad && r->o_nd == r->o_r + 1,
+          "replay record layout is not [s | a | s' | r | not_done]");
+  RingSide& g = P->rside;
+  g = RingSide{};
+  g.data = r->data;
+  g.rec = r->rec;
+  g.d_size = r->d_size;
+  g.idx_out = P->d_idx;
+  g.seed = r->seed;
+  g.ctr = h->d_ctr;
+  return 0;
 }
 
 static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_stats* stats) {
@@ -1647,7 +1734,7 @@ void td3_default_config(td3_config* c) {
   c->eps = 1e-8;
   c->seed = 0;
   c->device = 0;
-  c->use_graph = 1;
+  c->use_graph = 2;
   c->particles = 0;
   c->cdq = 1;
 }
@@ -1869,7 +1956,7 @@ int td3_train_step(td3_handle* h, rb_handle* rbh, int batch, void* stream, const
   TD3_ARG(!r->particles || (r->N == h->N && r->D == h->D), "particle shape does not match the learner");
   TD3_RC(ensure_plan(h, batch));
   Plan* P = h->plan.get();
-  bind_ring(h, r);
+  TD3_RC(bind_ring(h, r));
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
   TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
   if (inject_idx) {
@@ -2085,8 +2172,9 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   TD3_HIP(hipSetDevice(h->cfg.device));
   TD3_RC(ensure_plan(h, batch));
   Plan* P = h->plan.get();
-  bind_ring(h, r);
-  std::vector<Stage>& st = P->body[actor_phase ? 1 : 0][0];
+  TD3_RC(bind_ring(h, r));
+  const bool fused = !P->particles;              // stage 0 (the gather) runs inside F_fwd0
+  std::vector<Stage>& st = fused ? P->body_ring[actor_phase ? 1 : 0][0] : P->body[actor_phase ? 1 : 0][0];
   const int n = (int)st.size() + 1;
   TD3_ARG(max_stages >= n, "max_stages too small");
   std::vector<hipEvent_t> ev(n + 1);
@@ -2094,7 +2182,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   hipStream_t s = h->stream;
   TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
   TD3_HIP(hipEventRecord(ev[0], s));
-  TD3_RC(input_from_ring(h, r, P, false, s));
+  if (!fused) TD3_RC(input_from_ring(h, r, P, false, s));
   TD3_HIP(hipEventRecord(ev[1], s));
   for (int i = 0; i < (int)st.size(); ++i) {
     TD3_RC(st[i].run(s));
@@ -2104,7 +2192,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   h->stage_names.clear();
   h->stage_kernels.clear();
   h->stage_names.push_back("gather");
-  h->stage_kernels.push_back("td3::gather_kernel");
+  h->stage_kernels.push_back(fused ? "(fused into F_fwd0)" : "td3::gather_kernel");
   for (int i = 0; i < n; ++i) {
     TD3_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
     if (i) {
