@@ -124,6 +124,99 @@ __device__ __forceinline__ void ln_fwd_rows(float (&x)[RB][8], const float (&g)[
   }
 }
 
+// ---- packed-math LayerNorm rows for the GEMM prologues (VALU-bound: 2 waves per SIMD, 4 rows
+// per wave).  v_pk_{add,mul,fma}_f32 on float pairs, no per-element masks: they rely on the
+// layout invariant that pad columns (>= K) of the rows and of gamma / beta are exactly zero
+// (td3.hip HBM layout), and lanes past the row width load zeros (rv_load).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk2(const float (&v)[8], int q) { return f32x2{v[2 * q], v[2 * q + 1]}; }
+__device__ __forceinline__ f32x2 pkfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 splat2(float s) { return f32x2{s, s}; }
+
+// Real-column indicator of the lane's 8 columns (1 below K, 0 on pads), shared by a wave's rows.
+__device__ __forceinline__ void real_mask(float (&m)[8], int K, int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = rcol(lane, j) < K ? 1.f : 0.f;
+}
+
+// y = (x*rstd + (-mean*rstd))*gamma + beta (torch CPU order, fma-contracted); mean = sum/K,
+// var = sum (x - mean)^2 / K over the real columns (two-pass), rstd = v_rsq(var + eps).  Pads of
+// y come out exactly 0 (gamma, beta pads are 0).
+template <int RB>
+__device__ __forceinline__ void ln_fwd_rows_pk(float (&x)[RB][8], const float (&g)[8], const float (&bb)[8],
+                                               const float (&rm)[8], float invK, float (&mean)[RB],
+                                               float (&rstd)[RB]) {
+  float s[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const f32x2 a = (pk2(x[r], 0) + pk2(x[r], 1)) + (pk2(x[r], 2) + pk2(x[r], 3));
+    s[r] = a.x + a.y;
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r) mean[r] = wsum(s[r]) * invK;
+  f32x2 d[RB][4];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const f32x2 nm = splat2(-mean[r]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[r][q] = pkfma(nm, pk2(rm, q), pk2(x[r], q));
+    f32x2 v = d[r][0] * d[r][0];
+    v = pkfma(d[r][1], d[r][1], v);
+    v = pkfma(d[r][2], d[r][2], v);
+    v = pkfma(d[r][3], d[r][3], v);
+    s[r] = v.x + v.y;
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rstd[r] = __builtin_amdgcn_rsqf(wsum(s[r]) * invK + 1e-5f);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {       // torch's order: (x*rstd + (-mean*rstd))*gamma + beta
+    const f32x2 rs = splat2(rstd[r]), nb = splat2(-mean[r] * rstd[r]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x2 y = pkfma(pkfma(pk2(x[r], q), rs, nb), pk2(g, q), pk2(bb, q));
+      x[r][2 * q] = y.x;
+      x[r][2 * q + 1] = y.y;
+    }
+  }
+}
+
+// dZ = relu'(h) * LN_bwd(dU) as ln_bwd_rows<RB, true> (norm on), packed: gx = gu*gamma,
+// xhat = (h - mean)*rstd, dh = rstd*((gx - mean(gx)) - xhat*mean(gx*xhat)).  The pads need no
+// mask: gamma pads are 0 (so gx and the sums ignore them) and h pads are 0 (relu' clears dh).
+template <int RB>
+__device__ __forceinline__ void ln_bwd_rows_pk(float (&gu)[RB][8], const float (&h)[RB][8], const float (&g)[8],
+                                               const float (&mean)[RB], const float (&rstd)[RB], float invK) {
+  f32x2 gx[RB][4], xh[RB][4];
+  float s1[RB], s2[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const f32x2 rs = splat2(rstd[r]), nm = splat2(-mean[r]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      gx[r][q] = pk2(gu[r], q) * pk2(g, q);
+      xh[r][q] = (pk2(h[r], q) + nm) * rs;          // (h - mean)*rstd: no cancellation near the mean
+    }
+    const f32x2 a = (gx[r][0] + gx[r][1]) + (gx[r][2] + gx[r][3]);
+    f32x2 b = gx[r][0] * xh[r][0];
+    b = pkfma(gx[r][1], xh[r][1], b);
+    b = pkfma(gx[r][2], xh[r][2], b);
+    b = pkfma(gx[r][3], xh[r][3], b);
+    s1[r] = a.x + a.y;
+    s2[r] = b.x + b.y;
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const f32x2 m1 = splat2(wsum(s1[r]) * invK), nm2 = splat2(-(wsum(s2[r]) * invK));
+    const f32x2 rs = splat2(rstd[r]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x2 t = rs * pkfma(xh[r][q], nm2, gx[r][q] - m1);
+      gu[r][2 * q] = h[r][2 * q] > 0.f ? t.x : 0.f;
+      gu[r][2 * q + 1] = h[r][2 * q + 1] > 0.f ? t.y : 0.f;
+    }
+  }
+}
+
 // dZ = relu'(h) * LN_bwd(dU): gx = gu*gamma; dh = rstd*((gx - mean(gx)) - xhat*mean(gx*xhat)).
 // RELU = false: the LayerNorm input is not a ReLU output (TD3_particles lnorm1 on the
 // concatenated [pooled | features | action] row), so no relu' mask is applied.

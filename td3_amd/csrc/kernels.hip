@@ -29,6 +29,32 @@
 
 namespace td3 {
 
+// In-kernel phase timeline (experiment builds only: tools/build_exp.sh tl "-DTD3_TL"): per
+// workgroup, s_memrealtime (100 MHz) at entry / after the prologue barrier / after the MFMA
+// loop / after its own stores drained, plus the XCC id.  Read back with td3_tl_read.
+#ifdef TD3_TL
+__device__ unsigned long long td3_tl[8192][8];
+__device__ __forceinline__ void tl_mark(int k) {
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    if (k == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    td3_tl[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+    if (k == 0) {
+      unsigned x;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+      td3_tl[blockIdx.x][4] = x;
+    }
+  }
+}
+#define TL_MARK(k) tl_mark(k)
+#else
+#define TL_MARK(k)
+#endif
+#ifdef TD3_TL_FINE      // drain the loads at the mark (changes the overlap: phase attribution only)
+#define TL_FINE(k) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); TL_MARK(k); } while (0)
+#else
+#define TL_FINE(k)
+#endif
+
 __device__ __forceinline__ void lds_put_row(float* smem, int S, int row, int Kp, int lane, const float (&v)[8]) {
   lds_store8(smem + row * S, Kp, lane, v);
 }
@@ -55,7 +81,13 @@ __device__ __forceinline__ void pro_copy(const GemmProb& P, float* smem, const C
   }
 }
 
-__device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx& c) {
+struct NoOp {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+template <class AfterIssue = NoOp>
+__device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx& c,
+                                       const AfterIssue& after_issue = AfterIssue()) {
   constexpr int RB = kRPW;
   float x[RB][8], g[8], bb[8], mean[RB], rstd[RB];
 #pragma unroll
@@ -63,7 +95,12 @@ __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx
     rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r) * P.lda, P.Kp, c.lane);
   rv_load(g, P.lng, P.Kp, c.lane);
   rv_load(bb, P.lnb, P.Kp, c.lane);
-  ln_fwd_rows<RB>(x, g, bb, P.Kreal, c.lane, mean, rstd);
+  after_issue();
+  TL_FINE(6);
+  float rm[8];
+  real_mask(rm, P.Kreal, c.lane);
+  ln_fwd_rows_pk<RB>(x, g, bb, rm, 1.0f / (float)P.Kreal, mean, rstd);
+  TL_FINE(7);
   const bool t0 = c.nt == 0;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
@@ -93,7 +130,8 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
       mean[r] = P.norm ? gld(P.stats + (grow)) : 0.f;
       rstd[r] = P.norm ? gld(P.stats + (c.Bp + grow)) : 1.f;
     }
-    ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.Kreal, c.lane, P.norm);
+    if (P.norm) ln_bwd_rows_pk<RB>(gu, h, g, mean, rstd, 1.0f / (float)P.Kreal);
+    else ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.Kreal, c.lane, 0);
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       const int row = c.wave * kRPW + r0 + r;
@@ -637,6 +675,8 @@ __device__ __forceinline__ int xcd_tile(int nb) {
   return (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
 }
 
+
+
 template <int MODE, int WN, int PRO>
 __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, Counters* bump, int bump_actor,
                                                         int nb) {
@@ -647,6 +687,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   constexpr int OUTW = 32 * WN;                // output columns of the workgroup
   constexpr bool kPrefetchB = true;
   const int b = xcd_tile(nb);
+  TL_MARK(0);
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     bump->total_it += 1;                       // TD3_featured.py:124
     bump->critic_step += 1;
@@ -678,17 +719,29 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   // bias of the epilogue's column, requested with the weights (off the tail of the chain)
   const int bcol = (WK == 1) ? ncol : n0 + (int)(threadIdx.x % OUTW);
   const float bias = (MODE == 0 && P.bias && (WK > 1 ? bcol < P.Nout : active)) ? gld(P.bias + bcol) : 0.f;
-  if constexpr (kPrefetchB) {
+#ifdef TD3_AFIRST
+  constexpr bool kAFirst = PRO == kProLN;   // experiment: A rows requested ahead of the weights
+#else
+  constexpr bool kAFirst = false;
+#endif
+  if constexpr (kPrefetchB && !kAFirst) {
     load_b<MODE>(P, bv, cb, nch, ncol, h);
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
   }
+  TL_MARK(5);
 
   const Ctx c{m0, wave, lane, nt, Bp, S};
   if constexpr (PRO == kProCopy) pro_copy<kRPW>(P, smem, c);
+  else if constexpr (PRO == kProLN && kAFirst)
+    pro_ln(P, smem, c, [&]() {
+      load_b<MODE>(P, bv, cb, nch, ncol, h);
+      __builtin_amdgcn_sched_barrier(0);
+    });
   else if constexpr (PRO == kProLN) pro_ln(P, smem, c);
   else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
   else if constexpr (PRO == kProGather) pro_gather(P, tab.rs, smem, c, pi);
   __syncthreads();
+  TL_MARK(1);
 
   f32x16 acc;
 #pragma unroll
@@ -742,12 +795,14 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
         gst(P.C + ((size_t)(m0 + row) * P.ldc + col), v);
       }
     }
+    TL_MARK(2);
   } else {
     __syncthreads();
     float* red = smem;  // [kNW][32][33]; wave = wk * WN + wn
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
     __syncthreads();
+    TL_MARK(2);
 #pragma unroll
     for (int q = 0; q < 32 * OUTW / NT; ++q) {
       const int e = threadIdx.x + NT * q;
@@ -761,6 +816,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
       if (n0 + colw < P.Nout) gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + colw), v);
     }
   }
+  TL_MARK(3);
 }
 
 // ================================================================== act / eval_q heads
@@ -817,7 +873,8 @@ __global__ __launch_bounds__(256) void lnbwd_rows_kernel(const LnBwdProb* __rest
     mean[r] = norm ? gld(P.stats + (row0 + r)) : 0.f;
     rstd[r] = norm ? gld(P.stats + (Bp + row0 + r)) : 1.f;
   }
-  ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.K, lane, norm);
+  if (norm) ln_bwd_rows_pk<RB>(gu, h, g, mean, rstd, 1.0f / (float)P.K);
+  else ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.K, lane, 0);
 #pragma unroll
   for (int r = 0; r < RB; ++r) rv_store(P.GZ + (size_t)(row0 + r) * P.ld, P.ld, lane, gu[r]);
 }
@@ -1245,3 +1302,18 @@ int kernels_init() {
 }
 
 }  // namespace td3
+
+#ifdef TD3_TL
+// Experiment builds only: copy the gemm-stage timeline of the last launch (n workgroups).
+extern "C" int td3_tl_read(unsigned long long* out, int n) {
+  if (n > 8192) n = 8192;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(td3::td3_tl), (size_t)n * 8 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return 0;
+}
+extern "C" int td3_tl_clear() {
+  static unsigned long long z[8192][8];
+  return hipMemcpyToSymbol(HIP_SYMBOL(td3::td3_tl), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif

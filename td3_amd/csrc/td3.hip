@@ -1393,8 +1393,10 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
   // (tools/launch_floor.hip) but little host time; direct launches cost the host ~3 us each and
   // the GPU nothing extra.  While the last policy step is still queued the host is ahead of the
   // GPU, so its launch time is hidden: launch directly.  Otherwise (host-bound loops) replay.
+  // Data parallel (RCCL comm attached): auto launches directly, so every rank issues its
+  // all-reduces the same way whatever its local progress (no captured / uncaptured mix).
   const bool graph = h->cfg.use_graph == 1 ||
-                     (h->cfg.use_graph == 2 && hipEventQuery(h->actor_ev) != hipErrorNotReady);
+                     (h->cfg.use_graph == 2 && !h->comm && hipEventQuery(h->actor_ev) != hipErrorNotReady);
   if (!graph) {
     if (ring && !fused) TD3_RC(input_from_ring(h, ring, P, false, s));
     return run_stages(st, s);

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""In-kernel phase timeline of the GEMM stages of one HalfCheetah B=256 step (GPU box helper,
+not product code).  Needs the TD3_TL experiment build:
+
+    tools/build_exp.sh tl "-DTD3_TL"
+    TD3_LIB=tools/exp/libtd3hip_tl.so python3 tools/tl_probe.py
+
+Per stage: HIP-event time per launch (back-to-back), and from the per-workgroup s_memrealtime
+marks of one launch: the span first-entry -> last-drained-store, the entry spread, and the
+median prologue / MFMA / epilogue phases of a workgroup (µs)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+class Box:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+
+
+def main():
+    import torch
+    torch.cuda.set_device(0)
+    from td3_amd import _lib
+    from td3_amd.TD3_featured import TD3
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured as RB
+    lib = _lib.load()
+    lib.td3_tl_read.restype = C.c_int
+    lib.td3_tl_read.argtypes = [C.c_void_p, C.c_int]
+    lib.td3_tl_clear.restype = C.c_int
+    sd, ad, B = 17, 6, 256
+    pol = TD3(Box((sd,)), Box((ad,)), max_action=1.0, norm="layer", device=0, seed=17, use_graph=False)
+    rb = RB(Box((sd,)), Box((ad,)), max_size=100_000, device=0, seed=3)
+    rb.fill_synthetic(100_000, 1.0, seed=7)
+    for _ in range(20):
+        pol.train(rb, B)
+    pol.sync()
+    h = pol._h
+    ms = (C.c_float * 128)()
+    n = C.c_int()
+    buf = np.zeros((8192, 8), dtype=np.uint64)
+    for phase in (0, 1):
+        _lib.check(lib.td3_profile_stages(h, rb.handle, B, phase, ms, 128, C.byref(n)), "profile")
+        print(f"== phase {phase}")
+        print(f"{'stage':16s} {'kernel':28s} {'ev_us':>6s} {'nwg':>4s} {'span':>6s} {'spread':>6s} "
+              f"{'pro':>5s} {'mfma':>5s} {'epi':>5s} {'pro_max':>7s} {'end_max':>7s}")
+        for i in range(1, n.value):
+            name = lib.td3_stage_name(h, i).decode()
+            kern = lib.td3_stage_kernel(h, i).decode()
+            if name.endswith("_allreduce"):
+                continue
+            t = C.c_float()
+            _lib.check(lib.td3_time_stage(h, i, 20, C.byref(t)), "time")
+            ev = t.value * 1e3
+            if "gemm_kernel" not in kern:
+                print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f}")
+                continue
+            lib.td3_tl_clear()
+            _lib.check(lib.td3_time_stage(h, i, 1, C.byref(t)), "time1")
+            lib.td3_tl_read(buf.ctypes.data, 8192)
+            v = buf[(buf[:, 3] != 0)].astype(np.int64)
+            t0, t1, t2, t3 = v[:, 0], v[:, 1], v[:, 2], v[:, 3]
+            base = t0.min()
+            span = (t3.max() - base) * 0.01
+            spread = (t0.max() - base) * 0.01
+            pro = np.median(t1 - t0) * 0.01
+            mf = np.median(t2 - t1) * 0.01
+            ep = np.median(t3 - t2) * 0.01
+            print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f} {len(v):4d} {span:6.2f} {spread:6.2f} "
+                  f"{pro:5.2f} {mf:5.2f} {ep:5.2f} {(t1 - base).max() * 0.01:7.2f} {(t3 - base).max() * 0.01:7.2f}")
+            t5, t6, t7 = v[:, 5], v[:, 6], v[:, 7]
+            fine = f"   w_issued {np.median(t5 - t0) * 0.01:5.2f}"
+            if t6.min() > 0:
+                fine += f" rows_in {np.median(t6 - t0) * 0.01:5.2f} ln_done {np.median(t7 - t0) * 0.01:5.2f}"
+            print(fine)
+            if name in ("F_fwd1", "TF_fwd1") and phase == 1:
+                xcc = v[:, 4]
+                print("   per-XCC wg counts:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
+                q = np.percentile((t1 - t0) * 0.01, [10, 50, 90])
+                print("   prologue p10/50/90:", np.round(q, 2).tolist(),
+                      " entry p10/50/90:", np.round(np.percentile((t0 - base) * 0.01, [10, 50, 90]), 2).tolist())
+
+
+if __name__ == "__main__":
+    main()
