@@ -658,11 +658,11 @@ __device__ __forceinline__ void load_chunk(const GemmProb& P, float (&b)[16], in
   }
 }
 
-template <int MODE>
-__device__ __forceinline__ void load_b(const GemmProb& P, float (&bv)[kMaxChunks][16], int cb, int nch,
+template <int MODE, int NCH>
+__device__ __forceinline__ void load_b(const GemmProb& P, float (&bv)[NCH][16], int cb, int nch,
                                        int ncol, int h) {
 #pragma unroll
-  for (int cc = 0; cc < kMaxChunks; ++cc) load_chunk<MODE>(P, bv[cc], min(cb + cc, nch - 1), ncol, h);
+  for (int cc = 0; cc < NCH; ++cc) load_chunk<MODE>(P, bv[cc], min(cb + cc, nch - 1), ncol, h);
 }
 
 // XCD-aware tile order (cdna_hip_programming.md §5.5 T1): the dispatcher deals blocks
@@ -686,19 +686,27 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   constexpr int NT = 64 * kNW;                 // threads
   constexpr int OUTW = 32 * WN;                // output columns of the workgroup
   constexpr bool kPrefetchB = true;
+  // the problem directory in the same scalar-load batch as nb (one round trip, not two)
+  asm volatile("" ::"s"(nb), "s"(Bp), "s"(tab.nprob), "s"(tab.p[1].tile_begin), "s"(tab.p[2].tile_begin),
+               "s"(tab.p[3].tile_begin));
   const int b = xcd_tile(nb);
   TL_MARK(0);
-  if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
-    bump->total_it += 1;                       // TD3_featured.py:124
-    bump->critic_step += 1;
-    if (bump_actor) bump->actor_step += 1;
-  }
   if (b >= nb) return;
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < kMaxProbs; ++i)
     if (i < tab.nprob && b >= tab.p[i].tile_begin) pi = i;
   const GemmProb& P = tab.p[pi];
+  // Every kernel-argument field this workgroup reads, requested in ONE scalar-load batch: left
+  // to itself the compiler requests each where first used, a chain of ~4 dependent kernarg
+  // round trips (~1.1 us) ahead of the first operand load (tools/tl_probe.py).
+  asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.W), "s"(P.ldw), "s"(P.Nout),
+               "s"(P.C), "s"(P.ldc), "s"(P.relu), "s"(P.tile_begin), "s"(P.bias), "s"(P.lng), "s"(P.lnb),
+               "s"(P.stats), "s"(P.Aout), "s"(P.ldao), "s"(P.H), "s"(P.ldh), "s"(P.norm), "s"(P.B));
+  if constexpr (PRO == kProGather)
+    asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]),
+                 "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
+                 "s"(tab.rs.ctr));
   const int mtiles = Bp >> 5;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
@@ -715,33 +723,37 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   const bool active = ncol0 < P.Nout;
   const int ncol = (active ? ncol0 : 0) + i;
 
-  float bv[kMaxChunks][16];
+  // weight chunks requested at the kernel start (the rest stream in the MFMA loop).  Prefetching
+  // all 4 chunks of a WN=2 wave was no faster: the A-row loads then queue behind 16 weight loads.
+  constexpr int kCh = kMaxChunks;
+  float bv[kCh][16];
   // bias of the epilogue's column, requested with the weights (off the tail of the chain)
   const int bcol = (WK == 1) ? ncol : n0 + (int)(threadIdx.x % OUTW);
   const float bias = (MODE == 0 && P.bias && (WK > 1 ? bcol < P.Nout : active)) ? gld(P.bias + bcol) : 0.f;
-#ifdef TD3_AFIRST
-  constexpr bool kAFirst = PRO == kProLN;   // experiment: A rows requested ahead of the weights
-#else
-  constexpr bool kAFirst = false;
-#endif
-  if constexpr (kPrefetchB && !kAFirst) {
-    load_b<MODE>(P, bv, cb, nch, ncol, h);
+  if constexpr (kPrefetchB) {
+    load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
   }
   TL_MARK(5);
+  // WN >= 2 waves own more chunks than kCh: the next two are requested right behind the A rows
+  // (in flight during the LayerNorm, not queued ahead of it), the rest stream in the MFMA loop
+  float bs0[16], bs1[16];
+  const int s0 = cb + kCh;
+  auto issue_stream = [&]() {
+    if constexpr (WN >= 2) {
+      if (s0 < ce) load_chunk<MODE>(P, bs0, s0, ncol, h);
+      if (s0 + 1 < ce) load_chunk<MODE>(P, bs1, s0 + 1, ncol, h);
+    }
+  };
 
   const Ctx c{m0, wave, lane, nt, Bp, S};
   if constexpr (PRO == kProCopy) pro_copy<kRPW>(P, smem, c);
-  else if constexpr (PRO == kProLN && kAFirst)
-    pro_ln(P, smem, c, [&]() {
-      load_b<MODE>(P, bv, cb, nch, ncol, h);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  else if constexpr (PRO == kProLN) pro_ln(P, smem, c);
+  else if constexpr (PRO == kProLN) pro_ln(P, smem, c, issue_stream);
   else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
   else if constexpr (PRO == kProGather) pro_gather(P, tab.rs, smem, c, pi);
   __syncthreads();
   TL_MARK(1);
+  if constexpr (PRO != kProLN) issue_stream();
 
   f32x16 acc;
 #pragma unroll
@@ -749,7 +761,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   if (active) {
     const float* arow = smem + i * S + 16 * h;
 #pragma unroll
-    for (int cc = 0; cc < kMaxChunks; ++cc) {
+    for (int cc = 0; cc < kCh; ++cc) {
       if (cb + cc < ce) {
         const int kb = (cb + cc) * 32;
         float av[16];
@@ -762,23 +774,28 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
         for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[cc][s], acc);
       }
     }
-    // WN=4 on a wide K leaves this wave more than kMaxChunks chunks: the rest are streamed, the
-    // weights of chunk ch+1 in flight while chunk ch is multiplied
-    if (cb + kMaxChunks < ce) {
-      float bn[16];
-      load_chunk<MODE>(P, bn, cb + kMaxChunks, ncol, h);
-      for (int ch = cb + kMaxChunks; ch < ce; ++ch) {
-        float bc[16], av[16];
-#pragma unroll
-        for (int s = 0; s < 16; ++s) bc[s] = bn[s];
-        if (ch + 1 < ce) load_chunk<MODE>(P, bn, ch + 1, ncol, h);
+    // the streamed chunks: two buffers, chunk ch+2 requested as chunk ch is multiplied
+    if constexpr (WN >= 2) {
+      for (int ch = s0; ch < ce; ch += 2) {
+        float av[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float4 v = *reinterpret_cast<const float4*>(arow + ch * 32 + 4 * q);
           av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
         }
 #pragma unroll
-        for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bc[s], acc);
+        for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bs0[s], acc);
+        if (ch + 2 < ce) load_chunk<MODE>(P, bs0, ch + 2, ncol, h);
+        if (ch + 1 < ce) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(arow + (ch + 1) * 32 + 4 * q);
+            av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
+          }
+#pragma unroll
+          for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bs1[s], acc);
+          if (ch + 3 < ce) load_chunk<MODE>(P, bs1, ch + 3, ncol, h);
+        }
       }
     }
   }
@@ -817,6 +834,13 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
     }
   }
   TL_MARK(3);
+  // step counters (TD3_featured.py:124), off the head of the chain; the bumping stage never
+  // reads them (the sample of this step drew its rows in the stage before)
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
+    bump->total_it += 1;
+    bump->critic_step += 1;
+    if (bump_actor) bump->actor_step += 1;
+  }
 }
 
 // ================================================================== act / eval_q heads
