@@ -113,6 +113,11 @@ struct Counters {
   int64_t critic_step;  // critic Adam step (torch state['step'])
   int64_t actor_step;   // actor Adam step
   int64_t pad;
+  // beta^step of the Adam bias corrections (torch adam.py:531-533: 1 - beta**step), kept as running
+  // products by the step bump so no workgroup evaluates pow(): [0] beta1^critic_step,
+  // [1] beta2^critic_step, [2] beta1^actor_step, [3] beta2^actor_step
+  double pw[4];
+  double beta1, beta2;
 };
 
 }  // namespace td3

@@ -266,11 +266,19 @@ struct AdamK {
   float w1, b2, c2, bc2s, negss, eps, tau, omt, gscale;
 };
 
-__device__ __forceinline__ AdamK make_adam(const AdamArgs& a) {
+// beta1^step, beta2^step of the group (Counters::pw): request them early, build AdamK late.
+struct AdamPw {
+  double p1, p2;
+};
+__device__ __forceinline__ AdamPw adam_pw(const AdamArgs& a) {
+  const double* pw = a.ctr->pw + (a.which ? 2 : 0);
+  return AdamPw{pw[0], pw[1]};
+}
+
+__device__ __forceinline__ AdamK make_adam(const AdamArgs& a, const AdamPw& pw) {
   AdamK k;
-  const int64_t step = a.which ? a.ctr->actor_step : a.ctr->critic_step;
-  const double bc1 = 1.0 - pow(a.beta1, (double)step);
-  const double bc2 = 1.0 - pow(a.beta2, (double)step);
+  const double bc1 = 1.0 - pw.p1;
+  const double bc2 = 1.0 - pw.p2;
   k.negss = (float)(-(a.lr / bc1));
   k.bc2s = (float)sqrt(bc2);
   k.w1 = (float)(1.0 - a.beta1);
@@ -282,6 +290,8 @@ __device__ __forceinline__ AdamK make_adam(const AdamArgs& a) {
   k.gscale = a.grad_scale;
   return k;
 }
+
+__device__ __forceinline__ AdamK make_adam(const AdamArgs& a) { return make_adam(a, adam_pw(a)); }
 
 // torch _single_tensor_adam (adam.py:520-547): lerp, mul/addcmul, sqrt/div/add, addcdiv.
 __device__ __forceinline__ void adam_elem(float* __restrict__ p, float* __restrict__ m,

@@ -216,6 +216,7 @@ struct RowCtx {
 // exf[0]=max_action (1 for TD3_particles: tanh output, :68) exf[1]=policy_noise exf[2]=noise_clip
 constexpr int kHeadRegs = 8;   // head outputs kept in registers (wider heads loop)
 
+template <bool NORM>
 __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx& c) {
   const int K3 = P.exi[0], ld3 = P.exi[1], ldw4 = P.exi[2];
   const int ad = P.exi[5], sd = P.exi[6];
@@ -224,7 +225,7 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   float x[1][8], g[8], bb[8], mean[1], rstd[1];
   float w4[kHeadRegs][8], b4v[kHeadRegs];
   rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
-  if (P.norm) {
+  if (NORM) {
     rv_load(g, P.ex[1], ld3, c.lane);
     rv_load(bb, P.ex[2], ld3, c.lane);
   }
@@ -236,7 +237,7 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   }
   float nz = 0.f;
   if (target && !P.exi[4] && c.lane < ad) nz = gld(P.ex[5] + ((size_t)c.row * P.exi[7] + c.lane));
-  if (P.norm) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+  if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
   float mine = 0.f;                       // lane o keeps head output o
   float part[kHeadRegs];
 #pragma unroll
@@ -254,8 +255,8 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
     if (c.lane == o) mine = z;
   }
   if (!target) {
-    if (P.norm) rv_store(P.ex[8] + (size_t)c.row * ld3, ld3, c.lane, x[0]);
-    if (P.norm && c.lane == 0) {
+    if (NORM) rv_store(P.ex[8] + (size_t)c.row * ld3, ld3, c.lane, x[0]);
+    if (NORM && c.lane == 0) {
       gst(P.ex[9] + c.row, mean[0]);
       gst(P.ex[9] + (c.Bp + c.row), rstd[0]);
     }
@@ -291,6 +292,7 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
 // out: ex[17]=dZ4_j (ld 32) ex[18]=dU3_j ex[19]=U3_j ex[20]=stats3_j ex[21]=y ex[22]=sqerr_j
 //      ex[23]=Q_j  Aout=dZ3_j
 // exi[0]=K3 exi[1]=ld3 exi[2]=j   exf[0]=discount exf[1]=2/B
+template <bool NORM>
 __device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx& c) {
   const int K3 = P.exi[0], ld3 = P.exi[1], j = P.exi[2];
   float x0[1][8], x1[1][8], xq[1][8], h[1][8], g[3][8], bb[3][8], w[3][8];
@@ -299,7 +301,7 @@ __device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx&
   rv_load(xq[0], P.ex[2] + (size_t)c.row * ld3, ld3, c.lane);
 #pragma unroll
   for (int n = 0; n < 3; ++n) {
-    if (P.norm) {
+    if (NORM) {
       rv_load(g[n], P.ex[3 + n], ld3, c.lane);
       rv_load(bb[n], P.ex[6 + n], ld3, c.lane);
     }
@@ -310,7 +312,7 @@ __device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx&
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) h[0][jj] = xq[0][jj];
   float m0[1], s0[1], m1[1], s1[1], mq[1], sq[1];
-  if (P.norm) {
+  if (NORM) {
     ln_fwd_rows<1>(x0, g[0], bb[0], K3, c.lane, m0, s0);
     ln_fwd_rows<1>(x1, g[1], bb[1], K3, c.lane, m1, s1);
     ln_fwd_rows<1>(xq, g[2], bb[2], K3, c.lane, mq, sq);
@@ -328,7 +330,7 @@ __device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx&
     gst(P.ex[23] + c.row, q);
     gst(P.ex[22] + c.row, live ? d * d : 0.f);
     if (j == 0) gst(P.ex[21] + c.row, y);
-    if (P.norm) {
+    if (NORM) {
       gst(P.ex[20] + c.row, mq[0]);
       gst(P.ex[20] + (c.Bp + c.row), sq[0]);
     }
@@ -337,19 +339,20 @@ __device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx&
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) gu[0][jj] = gq * w[2][jj];
   rv_store(P.ex[18] + (size_t)c.row * ld3, ld3, c.lane, gu[0]);
-  if (P.norm) rv_store(P.ex[19] + (size_t)c.row * ld3, ld3, c.lane, xq[0]);
-  ln_bwd_rows<1>(gu, h, g[2], mq, sq, K3, c.lane, P.norm);
+  if (NORM) rv_store(P.ex[19] + (size_t)c.row * ld3, ld3, c.lane, xq[0]);
+  ln_bwd_rows<1>(gu, h, g[2], mq, sq, K3, c.lane, NORM);
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
 }
 
 // ---- actor loss -mean Q1(s, pi(s)) backward into LN3 of Q1 (:159) ------------------------
 // ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=w4 ex[4]=b4 out ex[5]=Q values, Aout=dZ3
 // exi[0]=K3 exi[1]=ld3   exf[0]=-1/B
+template <bool NORM>
 __device__ __forceinline__ void row_actor_loss(const GemmProb& P, const RowCtx& c) {
   const int K3 = P.exi[0], ld3 = P.exi[1];
   float x[1][8], h[1][8], g[8], bb[8], w[8], mean[1], rstd[1];
   rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
-  if (P.norm) {
+  if (NORM) {
     rv_load(g, P.ex[1], ld3, c.lane);
     rv_load(bb, P.ex[2], ld3, c.lane);
   }
@@ -357,14 +360,14 @@ __device__ __forceinline__ void row_actor_loss(const GemmProb& P, const RowCtx& 
   const float b4 = gld(P.ex[4]);
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) h[0][jj] = x[0][jj];
-  if (P.norm) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+  if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
   const float q = wsum(rv_pdot(x[0], w, K3, c.lane)) + b4;
   if (c.lane == 0) gst(P.ex[5] + c.row, q);
   const float gq = c.row < P.B ? P.exf[0] : 0.f;
   float gu[1][8];
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) gu[0][jj] = gq * w[jj];
-  ln_bwd_rows<1>(gu, h, g, mean, rstd, K3, c.lane, P.norm);
+  ln_bwd_rows<1>(gu, h, g, mean, rstd, K3, c.lane, NORM);
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
 }
 
@@ -374,6 +377,7 @@ __device__ __forceinline__ void row_actor_loss(const GemmProb& P, const RowCtx& 
 // out: ex[10]=dZ4 actor (ld 32) ex[11]=dU3 actor  Aout=dZ3 actor
 // exi[0]=K0 exi[1]=ld0 exi[2]=ldw1 exi[3]=sd exi[4]=ad exi[5]=K3 exi[6]=ld3 exi[7]=ldw4
 // exf[0]=max_action
+template <bool NORM>
 __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowCtx& c) {
   const int K0 = P.exi[0], ld0 = P.exi[1], ldw1 = P.exi[2], sd = P.exi[3], ad = P.exi[4];
   const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
@@ -383,7 +387,7 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
   rv_load(gu0[0], P.ex[0] + (size_t)c.row * ld0, ld0, c.lane);
   rv_load(h0[0], P.ex[1] + (size_t)c.row * ld0, ld0, c.lane);
   rv_load(h3[0], P.ex[7] + (size_t)c.row * ld3, ld3, c.lane);
-  if (P.norm) {
+  if (NORM) {
     rv_load(g0, P.ex[3], ld0, c.lane);
     rv_load(g3, P.ex[9], ld3, c.lane);
     mn0[0] = gld(P.ex[2] + c.row);
@@ -420,7 +424,7 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
     const int oo = o < ad ? o : 0;
     rv_load(w4[o], P.ex[6] + (size_t)oo * ldw4, ldw4, c.lane);
   }
-  ln_bwd_rows<1>(gu0, h0, g0, mn0, rs0, K0, c.lane, P.norm);       // dZ0 of Q1 (pads -> 0)
+  ln_bwd_rows<1>(gu0, h0, g0, mn0, rs0, K0, c.lane, NORM);       // dZ0 of Q1 (pads -> 0)
   const bool live = c.row < P.B;
   float gu3[1][8];
 #pragma unroll
@@ -454,7 +458,7 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
     for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4o[jj];
   }
   rv_store(P.ex[11] + (size_t)c.row * ld3, ld3, c.lane, gu3[0]);
-  ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, P.norm);        // dZ3 of the actor
+  ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, NORM);        // dZ3 of the actor
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
 }
 
@@ -468,6 +472,7 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
 // out: ex[17]=dZ4_j (ld 32) ex[18]=dU3_j ex[19]=U3_j ex[20]=stats3_j ex[21]=y [Bp][32]
 //      ex[22]=sqerr_j (sum over outputs) ex[23]=Q_j [Bp][32]   Aout=dZ3_j
 // exi[0]=K3 exi[1]=ld3 exi[2]=j exi[3]=nq exi[4]=ldw4 exi[5]=cdq   exf[0]=discount exf[1]=2/(B*nq)
+template <bool NORM>
 __device__ __forceinline__ void row_critic_loss_p(const GemmProb& P, const RowCtx& c) {
   const int K3 = P.exi[0], ld3 = P.exi[1], j = P.exi[2], nq = P.exi[3], ldw4 = P.exi[4];
   const bool cdq = P.exi[5] != 0;
@@ -475,7 +480,7 @@ __device__ __forceinline__ void row_critic_loss_p(const GemmProb& P, const RowCt
   rv_load(x0[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
   rv_load(x1[0], P.ex[1] + (size_t)c.row * ld3, ld3, c.lane);
   rv_load(xq[0], P.ex[2] + (size_t)c.row * ld3, ld3, c.lane);
-  if (P.norm) {
+  if (NORM) {
 #pragma unroll
     for (int n = 0; n < 3; ++n) {
       rv_load(g[n], P.ex[3 + n], ld3, c.lane);
@@ -486,7 +491,7 @@ __device__ __forceinline__ void row_critic_loss_p(const GemmProb& P, const RowCt
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) h[0][jj] = xq[0][jj];
   float m0[1], s0[1], m1[1], s1[1], mq[1], sq[1];
-  if (P.norm) {
+  if (NORM) {
     ln_fwd_rows<1>(x0, g[0], bb[0], K3, c.lane, m0, s0);
     ln_fwd_rows<1>(x1, g[1], bb[1], K3, c.lane, m1, s1);
     ln_fwd_rows<1>(xq, g[2], bb[2], K3, c.lane, mq, sq);
@@ -521,31 +526,32 @@ __device__ __forceinline__ void row_critic_loss_p(const GemmProb& P, const RowCt
   }
   if (c.lane == 0) {
     gst(P.ex[22] + c.row, se);
-    if (P.norm) {
+    if (NORM) {
       gst(P.ex[20] + c.row, mq[0]);
       gst(P.ex[20] + (c.Bp + c.row), sq[0]);
     }
   }
   rv_store(P.ex[18] + (size_t)c.row * ld3, ld3, c.lane, gu[0]);
-  if (P.norm) rv_store(P.ex[19] + (size_t)c.row * ld3, ld3, c.lane, xq[0]);
-  ln_bwd_rows<1>(gu, h, g[2], mq, sq, K3, c.lane, P.norm);
+  if (NORM) rv_store(P.ex[19] + (size_t)c.row * ld3, ld3, c.lane, xq[0]);
+  ln_bwd_rows<1>(gu, h, g[2], mq, sq, K3, c.lane, NORM);
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
 }
 
 // -mean over B*nq of Q1(s, pi(s)) (TD3_particles.py:211-212), head + LN3 backward of Q1.
 // ex[0]=H3 ex[1]=gamma3 ex[2]=beta3 ex[3]=W4 ex[4]=b4  out ex[5]=Q [Bp][32], Aout=dZ3
 // exi[0]=K3 exi[1]=ld3 exi[2]=nq exi[3]=ldw4   exf[0]=-1/(B*nq)
+template <bool NORM>
 __device__ __forceinline__ void row_actor_loss_p(const GemmProb& P, const RowCtx& c) {
   const int K3 = P.exi[0], ld3 = P.exi[1], nq = P.exi[2], ldw4 = P.exi[3];
   float x[1][8], h[1][8], g[8], bb[8], mean[1], rstd[1];
   rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
-  if (P.norm) {
+  if (NORM) {
     rv_load(g, P.ex[1], ld3, c.lane);
     rv_load(bb, P.ex[2], ld3, c.lane);
   }
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) h[0][jj] = x[0][jj];
-  if (P.norm) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+  if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
   const float gq = c.row < P.B ? P.exf[0] : 0.f;
   float gu[1][8];
 #pragma unroll
@@ -558,7 +564,7 @@ __device__ __forceinline__ void row_actor_loss_p(const GemmProb& P, const RowCtx
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) gu[0][jj] += gq * w[jj];
   }
-  ln_bwd_rows<1>(gu, h, g, mean, rstd, K3, c.lane, P.norm);
+  ln_bwd_rows<1>(gu, h, g, mean, rstd, K3, c.lane, NORM);
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
 }
 
@@ -569,6 +575,7 @@ __device__ __forceinline__ void row_actor_loss_p(const GemmProb& P, const RowCtx
 // ex[8]=stats3 (actor) ex[9]=gamma3 (actor)   out: ex[10]=dZ4 actor (ld 32) ex[11]=dU3 actor, Aout=dZ3
 // exi[0]=Kin exi[1]=ld_in exi[3]=first action column exi[4]=ad exi[5]=K3 exi[6]=ld3 exi[7]=ldw4
 // exf[0]=max_action scale of the policy output
+template <bool NORM>
 __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const RowCtx& c) {
   const int Kin = P.exi[0], ldin = P.exi[1], acol = P.exi[3], ad = P.exi[4];
   const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
@@ -577,7 +584,7 @@ __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const Ro
   rv_load(gu[0], P.ex[0] + (size_t)c.row * ldin, ldin, c.lane);
   rv_load(xr[0], P.ex[1] + (size_t)c.row * ldin, ldin, c.lane);
   rv_load(h3[0], P.ex[7] + (size_t)c.row * ld3, ld3, c.lane);
-  if (P.norm) {
+  if (NORM) {
     rv_load(gi, P.ex[3], ldin, c.lane);
     rv_load(g3, P.ex[9], ld3, c.lane);
     mi[0] = gld(P.ex[2] + c.row);
@@ -589,7 +596,7 @@ __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const Ro
     ri[0] = rs3[0] = 1.f;
   }
   const float tl = c.lane < ad ? gld(P.ex[5] + ((size_t)c.row * 32 + c.lane)) : 0.f;
-  ln_bwd_rows<1, false>(gu, xr, gi, mi, ri, Kin, c.lane, P.norm);     // grad of the Q input row
+  ln_bwd_rows<1, false>(gu, xr, gi, mi, ri, Kin, c.lane, NORM);     // grad of the Q input row
   const bool live = c.row < P.B;
   float gu3[1][8];
 #pragma unroll
@@ -610,22 +617,22 @@ __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const Ro
     for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4[jj];
   }
   rv_store(P.ex[11] + (size_t)c.row * ld3, ld3, c.lane, gu3[0]);
-  ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, P.norm);
+  ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, NORM);
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
 }
 
-template <int KIND>
+template <int KIND, bool NORM>
 __global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
   const GemmProb& P = tab.p[blockIdx.y];
   const RowCtx c{(int)(blockIdx.x * 4 + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
   if (c.row >= Bp) return;
-  if constexpr (KIND == kRowPolicyHead) row_policy_head(P, c);
-  else if constexpr (KIND == kRowCriticLoss) row_critic_loss(P, c);
-  else if constexpr (KIND == kRowActorLoss) row_actor_loss(P, c);
-  else if constexpr (KIND == kRowActorHeadBwd) row_actor_head_bwd(P, c);
-  else if constexpr (KIND == kRowCriticLossP) row_critic_loss_p(P, c);
-  else if constexpr (KIND == kRowActorLossP) row_actor_loss_p(P, c);
-  else if constexpr (KIND == kRowActorHeadBwdP) row_actor_head_bwd_p(P, c);
+  if constexpr (KIND == kRowPolicyHead) row_policy_head<NORM>(P, c);
+  else if constexpr (KIND == kRowCriticLoss) row_critic_loss<NORM>(P, c);
+  else if constexpr (KIND == kRowActorLoss) row_actor_loss<NORM>(P, c);
+  else if constexpr (KIND == kRowActorHeadBwd) row_actor_head_bwd<NORM>(P, c);
+  else if constexpr (KIND == kRowCriticLossP) row_critic_loss_p<NORM>(P, c);
+  else if constexpr (KIND == kRowActorLossP) row_actor_loss_p<NORM>(P, c);
+  else if constexpr (KIND == kRowActorHeadBwdP) row_actor_head_bwd_p<NORM>(P, c);
 }
 
 // ================================================================== batch-row GEMM stage
@@ -839,7 +846,13 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, C
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     bump->total_it += 1;
     bump->critic_step += 1;
-    if (bump_actor) bump->actor_step += 1;
+    bump->pw[0] *= bump->beta1;
+    bump->pw[1] *= bump->beta2;
+    if (bump_actor) {
+      bump->actor_step += 1;
+      bump->pw[2] *= bump->beta1;
+      bump->pw[3] *= bump->beta2;
+    }
   }
 }
 
@@ -907,9 +920,34 @@ __global__ __launch_bounds__(256) void lnbwd_rows_kernel(const LnBwdProb* __rest
 // N optimizer updates at once: every P/M/V(/T) load is issued before the first store, so the
 // element chain costs one memory round trip instead of N (the stores of one element could alias
 // the next element's loads for the compiler).
+// The optimizer state of N elements (P, M, V and, with Polyak, T), requested without waiting.
 template <int N>
-__device__ __forceinline__ void apply_grads(const DwArgs& a, const AdamK& k, const int64_t (&idx)[N],
-                                            const float (&g)[N], const bool (&ok)[N]) {
+struct AdamState {
+  float mm[N], vv[N], pp[N], tt[N];
+};
+template <int N>
+__device__ __forceinline__ void adam_state_load(const DwArgs& a, const int64_t (&idx)[N], const bool (&ok)[N],
+                                                AdamState<N>& st) {
+  if (a.mode == kDwGrad) return;
+  const bool pol = a.mode == kDwAdamPolyak;
+  int64_t any = -1;                                 // a valid index for the masked lanes' loads
+#pragma unroll
+  for (int e = N - 1; e >= 0; --e)
+    if (ok[e]) any = idx[e];
+  if (any < 0) return;
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    const int64_t j = ok[e] ? idx[e] : any;
+    st.mm[e] = gld(a.adam.M + j);
+    st.vv[e] = gld(a.adam.V + j);
+    st.pp[e] = gld(a.adam.P + j);
+    st.tt[e] = pol ? gld(a.adam.T + j) : 0.f;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void apply_grads_loaded(const DwArgs& a, const AdamK& k, const int64_t (&idx)[N],
+                                                   const float (&g)[N], const bool (&ok)[N], AdamState<N>& st) {
   if (a.mode == kDwGrad) {
 #pragma unroll
     for (int e = 0; e < N; ++e)
@@ -917,20 +955,10 @@ __device__ __forceinline__ void apply_grads(const DwArgs& a, const AdamK& k, con
     return;
   }
   const bool pol = a.mode == kDwAdamPolyak;
-  int64_t any = -1;                                 // a valid index for the masked lanes' loads
-#pragma unroll
-  for (int e = N - 1; e >= 0; --e)
-    if (ok[e]) any = idx[e];
-  if (any < 0) return;
-  float mm[N], vv[N], pp[N], tt[N];
-#pragma unroll
-  for (int e = 0; e < N; ++e) {
-    const int64_t j = ok[e] ? idx[e] : any;
-    mm[e] = gld(a.adam.M + j);
-    vv[e] = gld(a.adam.V + j);
-    pp[e] = gld(a.adam.P + j);
-    tt[e] = pol ? gld(a.adam.T + j) : 0.f;
-  }
+  float (&mm)[N] = st.mm;
+  float (&vv)[N] = st.vv;
+  float (&pp)[N] = st.pp;
+  float (&tt)[N] = st.tt;
 #pragma unroll
   for (int e = 0; e < N; ++e) {                    // torch _single_tensor_adam, as adam_elem
     mm[e] = __fmaf_rn(k.w1, g[e] - mm[e], mm[e]);
@@ -950,6 +978,14 @@ __device__ __forceinline__ void apply_grads(const DwArgs& a, const AdamK& k, con
   }
 }
 
+template <int N>
+__device__ __forceinline__ void apply_grads(const DwArgs& a, const AdamK& k, const int64_t (&idx)[N],
+                                            const float (&g)[N], const bool (&ok)[N]) {
+  AdamState<N> st;
+  adam_state_load<N>(a, idx, ok, st);
+  apply_grads_loaded<N>(a, k, idx, g, ok, st);
+}
+
 __device__ __forceinline__ void dw_load_chunk(const DwProb& P, int rc, int h, int n0, int k0, int i,
                                               float (&av)[16], float (&bv)[16]) {
   const int rb = rc * 32 + 16 * h;
@@ -962,10 +998,10 @@ __device__ __forceinline__ void dw_load_chunk(const DwProb& P, int rc, int h, in
   }
 }
 
-// Vector tile j of a problem: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU over 32 columns
-// (NT/32 row groups of 8-row strides), then the optimizer update of those 32 columns.
+// dw64_kernel's vector tile (Bp >= 512): one column per thread, NT/32 row groups of 8-row strides
+// (the float4 form below measured slower there: Humanoid C_dw 52 -> 61 us).
 template <int NT>
-__device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P, const AdamK& k, int j,
+__device__ __forceinline__ void dw_vector_tile_cols(const DwArgs& a, const DwProb& P, const AdamK& k, int j,
                                                float* red) {
   constexpr int NG = NT / 32;
   const int n0 = j * 32;
@@ -1018,13 +1054,86 @@ __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P,
   }
 }
 
+// Vector tile j of a problem: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU over 32 columns,
+// then the optimizer update of those 32 columns.  A thread owns 4 adjacent columns (float4 loads)
+// of every (NT/8)-th row: at Bp = 256 all of a thread's rows are requested in one batch, and the
+// optimizer state of the 32 x 3 elements is requested behind them.
+template <int NT>
+__device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P, const AdamPw& pw, int j,
+                                               float* red) {
+  constexpr int RG = NT / 8;                        // row groups
+  constexpr int U = 8;                              // rows per group and batch
+  const int n0 = j * 32;
+  const int c4 = (threadIdx.x & 7) * 4, rg = threadIdx.x >> 3;
+  const bool ln = P.offg >= 0;
+  const bool hasb = P.offb >= 0;                    // false: a LayerNorm-only problem (lnorm1)
+  const int c = threadIdx.x & 31;
+  const int64_t idx[3] = {P.offb + n0 + c, P.offg + n0 + c, P.offbeta + n0 + c};
+  const bool ok[3] = {hasb, ln, ln};
+  AdamState<3> st;
+  float sb[4] = {0.f, 0.f, 0.f, 0.f}, sg[4] = {0.f, 0.f, 0.f, 0.f}, sbeta[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r0 = rg; r0 < a.Bp; r0 += RG * U) {
+    float4 gz[U], gu[U], hh[U];
+    float mu[U], rs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = min(r0 + RG * u, a.Bp - 1);     // clamped: loads stay unconditional
+      gz[u] = hasb ? gld4(P.G + ((size_t)r * P.ldg + n0 + c4)) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ln) {
+        gu[u] = gld4(P.GU + ((size_t)r * P.ldgu + n0 + c4));
+        hh[u] = gld4(P.H + ((size_t)r * P.ldh + n0 + c4));
+        mu[u] = gld(P.stats + r);
+        rs[u] = gld(P.stats + (a.Bp + r));
+      }
+    }
+    if (r0 == rg && threadIdx.x < 32) adam_state_load<3>(a, idx, ok, st);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r0 + RG * u >= a.Bp) continue;
+      const float z[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
+      sb[0] += z[0]; sb[1] += z[1]; sb[2] += z[2]; sb[3] += z[3];
+      if (ln) {
+        const float g4[4] = {gu[u].x, gu[u].y, gu[u].z, gu[u].w};
+        const float h4[4] = {hh[u].x, hh[u].y, hh[u].z, hh[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sg[e] += g4[e] * ((h4[e] - mu[u]) * rs[u]);
+          sbeta[e] += g4[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[(0 * RG + rg) * 33 + c4 + e] = sb[e];
+    red[(1 * RG + rg) * 33 + c4 + e] = sg[e];
+    red[(2 * RG + rg) * 33 + c4 + e] = sbeta[e];
+  }
+  __syncthreads();
+  TL_MARK(1);
+  TL_MARK(2);
+  if (threadIdx.x < 32) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+    for (int g = 0; g < RG; ++g) {
+      s0 += red[(0 * RG + g) * 33 + c];
+      s1 += red[(1 * RG + g) * 33 + c];
+      s2 += red[(2 * RG + g) * 33 + c];
+    }
+    const float gq[3] = {s0, s1, s2};
+    apply_grads_loaded<3>(a, make_adam(a.adam, pw), idx, gq, ok, st);
+  }
+  TL_MARK(3);
+}
+
 // Matrix tiles: dW[n][k] = sum_r dZ[r][n] * U[r][k] (32x32 per workgroup, rows split over the
 // 4 waves, operands of the next row chunk in flight while the current one is multiplied).
 // Vector tiles: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU over 32 columns.
 // Both end in the fused optimizer update of the elements they own.
-__global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
+__global__ __launch_bounds__(256, 3) void dw_kernel(DwArgs a, int nb) {
   __shared__ float red[4 * 32 * 33];
   const int b = xcd_tile(nb);
+  TL_MARK(0);
   if (b >= nb) return;
   int pi = 0;
 #pragma unroll
@@ -1033,7 +1142,7 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
   const DwProb& P = a.probs[pi];
   const int t = b - P.tile_begin;
   const int nmat = (P.Np >> 5) * P.ntk;
-  const AdamK k = make_adam(a.adam);
+  const AdamPw pw = adam_pw(a.adam);            // requested now, used after the MFMA loop
   if (t < nmat) {
     const int kt = t % P.ntk, nt = t / P.ntk;
     const int n0 = nt * 32, k0 = kt * 32;
@@ -1046,21 +1155,36 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     float a0[16], b0[16], a1[16], b1[16];
     if (cb < ce) dw_load_chunk(P, cb, h, n0, k0, i, a0, b0);
+    if (cb + 1 < ce) dw_load_chunk(P, cb + 1, h, n0, k0, i, a1, b1);
+    // the optimizer state of this thread's 4 elements, requested behind the first two operand
+    // chunks (their MFMA waits do not include it) and landing during the MFMA chain
+    int64_t idx[4];
+    bool ok[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = threadIdx.x + 256 * q;
+      idx[q] = P.offW + (int64_t)(n0 + (e >> 5)) * P.Kp + k0 + (e & 31);
+      ok[q] = true;
+    }
+    AdamState<4> st;
+    adam_state_load<4>(a, idx, ok, st);
     for (int rc = cb; rc < ce; rc += 2) {
-      if (rc + 1 < ce) dw_load_chunk(P, rc + 1, h, n0, k0, i, a1, b1);
 #pragma unroll
       for (int s = 0; s < 16; ++s) acc = mfma32x32x2(a0[s], b0[s], acc);
-      if (rc + 1 >= ce) break;
       if (rc + 2 < ce) dw_load_chunk(P, rc + 2, h, n0, k0, i, a0, b0);
+      if (rc + 1 >= ce) break;
 #pragma unroll
       for (int s = 0; s < 16; ++s) acc = mfma32x32x2(a1[s], b1[s], acc);
+      if (rc + 3 < ce) dw_load_chunk(P, rc + 3, h, n0, k0, i, a1, b1);
     }
+    TL_MARK(5);
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
     __syncthreads();
-    int64_t idx[4];
+    TL_MARK(1);
+    TL_MARK(2);
+    const AdamK k = make_adam(a.adam, pw);
     float gq[4];
-    bool ok[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = threadIdx.x + 256 * q;
@@ -1068,14 +1192,13 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(DwArgs a, int nb) {
       float g = red[n * 33 + kk];
 #pragma unroll
       for (int w = 1; w < 4; ++w) g = g + red[(w * 32 + n) * 33 + kk];
-      idx[q] = P.offW + (int64_t)(n0 + n) * P.Kp + k0 + kk;
       gq[q] = g;
-      ok[q] = true;
     }
-    apply_grads<4>(a, k, idx, gq, ok);
+    apply_grads_loaded<4>(a, k, idx, gq, ok, st);
+    TL_MARK(3);
     return;
   }
-  dw_vector_tile<256>(a, P, k, t - nmat, red);
+  dw_vector_tile<256>(a, P, pw, t - nmat, red);
 }
 
 // Large batches (Bp >= 512): 64x64 weight tiles per workgroup of 8 waves.  Each step stages 64
@@ -1099,7 +1222,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   const int nmat = ntn * P.ntk;                      // ntk = k tiles of 64 in this mode
   const AdamK k = make_adam(a.adam);
   if (t >= nmat) {
-    dw_vector_tile<512>(a, P, k, t - nmat, sm);
+    dw_vector_tile_cols<512>(a, P, k, t - nmat, sm);
     return;
   }
   const int kt = t % P.ntk, nt = t / P.ntk;
@@ -1244,24 +1367,36 @@ int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int 
   return 0;
 }
 
-int launch_rows(int kind, const GemmTable& d, int Bp, hipStream_t s) {
+template <bool NORM>
+static void launch_rows_t(int kind, const GemmTable& d, int Bp, hipStream_t s) {
   const dim3 grid(Bp / 4, d.nprob);
   switch (kind) {
-    case kRowPolicyHead: hipLaunchKernelGGL(row_kernel<kRowPolicyHead>, grid, dim3(256), 0, s, d, Bp); break;
-    case kRowCriticLoss: hipLaunchKernelGGL(row_kernel<kRowCriticLoss>, grid, dim3(256), 0, s, d, Bp); break;
-    case kRowActorLoss: hipLaunchKernelGGL(row_kernel<kRowActorLoss>, grid, dim3(256), 0, s, d, Bp); break;
+    case kRowPolicyHead: hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(256), 0, s, d, Bp); break;
+    case kRowCriticLoss: hipLaunchKernelGGL((row_kernel<kRowCriticLoss, NORM>), grid, dim3(256), 0, s, d, Bp); break;
+    case kRowActorLoss: hipLaunchKernelGGL((row_kernel<kRowActorLoss, NORM>), grid, dim3(256), 0, s, d, Bp); break;
     case kRowActorHeadBwd:
-      hipLaunchKernelGGL(row_kernel<kRowActorHeadBwd>, grid, dim3(256), 0, s, d, Bp);
+      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(256), 0, s, d, Bp);
       break;
-    case kRowCriticLossP: hipLaunchKernelGGL(row_kernel<kRowCriticLossP>, grid, dim3(256), 0, s, d, Bp); break;
-    case kRowActorLossP: hipLaunchKernelGGL(row_kernel<kRowActorLossP>, grid, dim3(256), 0, s, d, Bp); break;
+    case kRowCriticLossP:
+      hipLaunchKernelGGL((row_kernel<kRowCriticLossP, NORM>), grid, dim3(256), 0, s, d, Bp);
+      break;
+    case kRowActorLossP: hipLaunchKernelGGL((row_kernel<kRowActorLossP, NORM>), grid, dim3(256), 0, s, d, Bp); break;
     case kRowActorHeadBwdP:
-      hipLaunchKernelGGL(row_kernel<kRowActorHeadBwdP>, grid, dim3(256), 0, s, d, Bp);
+      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwdP, NORM>), grid, dim3(256), 0, s, d, Bp);
       break;
-    default:
-      set_error("launch_rows: unknown kind %d", kind);
-      return -1;
+    default: break;
   }
+}
+
+// norm is a template parameter of the row kernels: with it a runtime flag, every LayerNorm operand
+// load sat in its own basic block and the scheduler issued the row's loads in ~6 dependent rounds.
+int launch_rows(int kind, const GemmTable& d, int Bp, hipStream_t s) {
+  if (kind < kRowPolicyHead || kind > kRowActorHeadBwdP) {
+    set_error("internal: unknown row kernel %d", kind);
+    return -1;
+  }
+  if (d.p[0].norm) launch_rows_t<true>(kind, d, Bp, s);
+  else launch_rows_t<false>(kind, d, Bp, s);
   TD3_HIP(hipGetLastError());
   return 0;
 }

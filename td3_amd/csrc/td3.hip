@@ -1741,6 +1741,21 @@ void td3_default_config(td3_config* c) {
   c->cdq = 1;
 }
 
+// Device counters with the Adam bias-correction powers at these steps (Python's beta ** step).
+static Counters make_counters(const td3_handle* h, int64_t total_it, int64_t critic_step, int64_t actor_step) {
+  Counters c{};
+  c.total_it = total_it;
+  c.critic_step = critic_step;
+  c.actor_step = actor_step;
+  c.beta1 = h->cfg.beta1;
+  c.beta2 = h->cfg.beta2;
+  c.pw[0] = std::pow(c.beta1, (double)critic_step);
+  c.pw[1] = std::pow(c.beta2, (double)critic_step);
+  c.pw[2] = std::pow(c.beta1, (double)actor_step);
+  c.pw[3] = std::pow(c.beta2, (double)actor_step);
+  return c;
+}
+
 int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_ARG(cfg && out, "null argument");
   TD3_ARG(cfg->state_dim > 0 && cfg->action_dim > 0, "dims must be positive");
@@ -1805,7 +1820,10 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
     g->G = p; p += g->size;
   }
   TD3_HIP(hipMalloc(&h->d_ctr, sizeof(Counters)));
-  TD3_HIP(hipMemset(h->d_ctr, 0, sizeof(Counters)));
+  {
+    const Counters c0 = make_counters(h, 0, 0, 0);
+    TD3_HIP(hipMemcpy(h->d_ctr, &c0, sizeof(c0), hipMemcpyHostToDevice));
+  }
   TD3_HIP(hipDeviceSynchronize());          // null-stream memsets vs the handle's non-blocking streams
   TD3_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   TD3_HIP(hipStreamCreateWithFlags(&h->act_stream, hipStreamNonBlocking));
@@ -1937,7 +1955,7 @@ int td3_set_counters(td3_handle* h, int64_t total_it, int64_t critic_step, int64
   TD3_ARG(total_it >= 0 && critic_step >= 0 && actor_step >= 0, "negative counter");
   TD3_HIP(hipSetDevice(h->cfg.device));
   TD3_HIP(hipStreamSynchronize(h->stream));
-  Counters c{total_it, critic_step, actor_step, 0};
+  const Counters c = make_counters(h, total_it, critic_step, actor_step);
   TD3_HIP(hipMemcpy(h->d_ctr, &c, sizeof(c), hipMemcpyHostToDevice));
   h->total_it = total_it;
   h->critic_step = critic_step;

@@ -57,7 +57,7 @@ def main():
             t = C.c_float()
             _lib.check(lib.td3_time_stage(h, i, 20, C.byref(t)), "time")
             ev = t.value * 1e3
-            if "gemm_kernel" not in kern:
+            if "gemm_kernel" not in kern and kern != "td3::dw_kernel":
                 print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f}")
                 continue
             lib.td3_tl_clear()
@@ -74,14 +74,16 @@ def main():
             print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f} {len(v):4d} {span:6.2f} {spread:6.2f} "
                   f"{pro:5.2f} {mf:5.2f} {ep:5.2f} {(t1 - base).max() * 0.01:7.2f} {(t3 - base).max() * 0.01:7.2f}")
             t5, t6, t7 = v[:, 5], v[:, 6], v[:, 7]
-            fine = f"   w_issued {np.median(t5 - t0) * 0.01:5.2f}"
+            fine = f"   mark5 {np.median(t5 - t0) * 0.01:5.2f}"
             if t6.min() > 0:
                 fine += f" rows_in {np.median(t6 - t0) * 0.01:5.2f} ln_done {np.median(t7 - t0) * 0.01:5.2f}"
             print(fine)
-            if name in ("F_fwd1", "TF_fwd1") and phase == 1:
+            if name in ("F_fwd1", "TF_fwd1", "C_dw") and phase == 1:
                 xcc = v[:, 4]
                 print("   per-XCC wg counts:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
                 q = np.percentile((t1 - t0) * 0.01, [10, 50, 90])
+                print("   end p10/50/90/max:", np.round(np.percentile((t3 - base) * 0.01, [10, 50, 90, 100]), 2).tolist(),
+                      " dur p10/50/90/max:", np.round(np.percentile((t3 - t0) * 0.01, [10, 50, 90, 100]), 2).tolist())
                 print("   prologue p10/50/90:", np.round(q, 2).tolist(),
                       " entry p10/50/90:", np.round(np.percentile((t0 - base) * 0.01, [10, 50, 90]), 2).tolist())
 
