@@ -185,6 +185,10 @@ struct Plan {
   // featured replay-ring bodies: the sample fused into F_fwd0 (kProGather), ring bound in rside
   std::vector<Stage> body_ring[2][2];
   RingSide rside{};
+  // the sample runs inside F_fwd0 only for short records: each F_fwd0 workgroup re-reads its
+  // rows' records, a loss once they are KBs (Humanoid: gather 4.8 + F_fwd0 23 us separate vs
+  // 34 us fused)
+  bool fuse_gather = false;
   hipGraphExec_t graph[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   // the same bodies with the replay-ring gather captured in front (Philox draw path)
   hipGraphExec_t graph_g[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -695,6 +699,7 @@ static int build_step(td3_handle* h, int B) {
   const int sd = h->sd, ad = h->ad;
   P->ld_s = pad32(sd);
   P->ld_sa = pad32(sd + ad);
+  P->fuse_gather = 2 * sd + ad + 2 <= 128;
   const NetL& an = h->actor.nets[0];
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[1];
@@ -1386,7 +1391,7 @@ static int input_from_batch(td3_handle* h, Plan* P, const float* s, const float*
 // launched first and, in graph mode, captured into the same hipGraph (one replay per step).
 static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring* ring) {
   Plan* P = h->plan.get();
-  const bool fused = ring && !P->particles;      // featured: the sample runs inside F_fwd0
+  const bool fused = ring && P->fuse_gather;     // featured: the sample runs inside F_fwd0
   std::vector<Stage>& st = fused ? P->body_ring[actor_phase][inj] : P->body[actor_phase][inj];
   h->last_body = &st;
   // use_graph 2 (auto): a hipGraph replay costs ~8 us of GPU time on top of its kernels
@@ -2193,7 +2198,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   TD3_RC(ensure_plan(h, batch));
   Plan* P = h->plan.get();
   TD3_RC(bind_ring(h, r));
-  const bool fused = !P->particles;              // stage 0 (the gather) runs inside F_fwd0
+  const bool fused = P->fuse_gather;             // stage 0 (the gather) runs inside F_fwd0
   std::vector<Stage>& st = fused ? P->body_ring[actor_phase ? 1 : 0][0] : P->body[actor_phase ? 1 : 0][0];
   const int n = (int)st.size() + 1;
   TD3_ARG(max_stages >= n, "max_stages too small");

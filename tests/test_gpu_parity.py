@@ -204,10 +204,13 @@ def test_foreign_buffer_path():
     _params_close(pol.critic.numpy_dict(), L.critic, 1e-4, "critic")
 
 
-def test_philox_graph_path_teacher_forced():
+@pytest.mark.parametrize("name", ["hc_layer", "hum_layer"])
+def test_philox_graph_path_teacher_forced(name):
     """The production path (Philox draws, gather captured in the step graph): the rows and
-    noise it drew are read back, the oracle replays the same step, and the results agree."""
-    S = featured_setup("hc_layer")
+    noise it drew are read back, the oracle replays the same step, and the results agree.
+    HalfCheetah records are sampled inside the first layer (kProGather); Humanoid's 3 KB
+    records by the separate gather kernel (td3.hip Plan::fuse_gather)."""
+    S = featured_setup(name)
     pol, rb = _make(S)
     L = orc.Learner(S["actor"], S["critic"], **S["kw"])
     seen = set()
