@@ -18,7 +18,9 @@ OUT = os.path.join(HERE, "libtd3hip.so")
 SOURCES = ["csrc/replay.hip", "csrc/kernels.hip", "csrc/encoder.hip", "csrc/td3.hip"]
 ARCH = os.environ.get("TD3_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
-         "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value"]
+         "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value",
+         # the GEMM stages' problem directory (first 6 int kernel arguments) arrives in SGPRs
+         "-mllvm", "-amdgpu-kernarg-preload-count=6"]
 
 
 def _hipcc():

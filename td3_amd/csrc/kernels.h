@@ -42,21 +42,29 @@ enum RowKind : int {
 constexpr int kMaxEx = 24;
 
 struct GemmProb {
-  const float* A; int lda;        // batch rows of the A side (kProCopy / kProLN / kProLNBwd)
-  int Kreal, Kp;                  // reduction length (real / padded to 32), Kp <= 512
+  // The first 128 bytes (pointers, then ints, no implicit padding) are everything a GEMM
+  // workgroup reads before its operand loads: gemm_kernel requests all of them in one scalar batch.
+  const float* A;                 // batch rows of the A side (kProCopy / kProLN / kProLNBwd)
   const float* lng; const float* lnb;   // LayerNorm affine of the A-side features
-  const float* H; int ldh;        // kProLNBwd: post-ReLU activations of the A side
+  const float* H;                 // kProLNBwd: post-ReLU activations of the A side
   float* stats;                   // [2][Bp] (mean, rstd): written by kProLN (n-tile 0), read by kProLNBwd
-  float* Aout; int ldao;          // nullable: n-tile 0 stores pro(A) rows (U_{l-1} or dZ_l)
-  const float* W; int ldw;
+  float* Aout;                    // nullable: n-tile 0 stores pro(A) rows (U_{l-1} or dZ_l)
+  const float* W;
   const float* bias;              // MODE 0, nullable
+  float* C;
+  int lda;
+  int Kreal, Kp;                  // reduction length (real / padded to 32), Kp <= 512
+  int ldh;
+  int ldao;
+  int ldw;
   int Nout;                       // padded output width (multiple of 32)
-  float* C; int ldc;
+  int ldc;
   int relu;
   int ntiles;                     // output column tiles of 32*WN
-  int tile_begin;                 // first flat workgroup id of this problem
+  int tile_begin;                 // first flat workgroup id of this problem (row kernels: unused)
   int norm;                       // LayerNorm present (norm="layer")
   int B;                          // real batch rows (rows >= B are padding)
+  int hot_pad;
   // head-prologue operands (meaning per kind: see the prologue functions in kernels.hip)
   float* ex[kMaxEx];
   int exi[12];

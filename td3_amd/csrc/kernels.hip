@@ -35,13 +35,14 @@ namespace td3 {
 #ifdef TD3_TL
 __device__ unsigned long long td3_tl[8192][8];
 __device__ __forceinline__ void tl_mark(int k) {
-  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+  const unsigned id = blockIdx.x + blockIdx.y * gridDim.x;
+  if (threadIdx.x == 0 && id < 8192) {
     if (k == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    td3_tl[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+    td3_tl[id][k] = __builtin_amdgcn_s_memrealtime();
     if (k == 0) {
       unsigned x;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-      td3_tl[blockIdx.x][4] = x;
+      td3_tl[id][4] = x;
     }
   }
 }
@@ -624,8 +625,9 @@ __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const Ro
 template <int KIND, bool NORM>
 __global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
   const GemmProb& P = tab.p[blockIdx.y];
+  // grid.x = Bp / 4 exactly (launch_rows): every wave owns a row, no bounds check (which would put
+  // a kernel-argument round trip ahead of the row's loads)
   const RowCtx c{(int)(blockIdx.x * 4 + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
-  if (c.row >= Bp) return;
   if constexpr (KIND == kRowPolicyHead) row_policy_head<NORM>(P, c);
   else if constexpr (KIND == kRowCriticLoss) row_critic_loss<NORM>(P, c);
   else if constexpr (KIND == kRowActorLoss) row_actor_loss<NORM>(P, c);
@@ -684,32 +686,34 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 
 
 
+// Kernel arguments: the problem directory (nb, nprob, tile_begin of problems 1..3, Bp) comes
+// first and is preloaded into SGPRs at wave launch (-amdgpu-kernarg-preload-count, build.py), so
+// the problem select costs no memory round trip; the problem's fields are then the first and only
+// kernel-argument round trip ahead of the operand loads.
 template <int MODE, int WN, int PRO>
-__global__ __launch_bounds__(64 * kNW) void gemm_kernel(GemmTable tab, int Bp, Counters* bump, int bump_actor,
-                                                        int nb) {
+__global__ __launch_bounds__(64 * kNW) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
+                                                        GemmTable tab, Counters* bump, int bump_actor) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
   constexpr int WK = kNW / WN;
   constexpr int NT = 64 * kNW;                 // threads
   constexpr int OUTW = 32 * WN;                // output columns of the workgroup
   constexpr bool kPrefetchB = true;
-  // the problem directory in the same scalar-load batch as nb (one round trip, not two)
-  asm volatile("" ::"s"(nb), "s"(Bp), "s"(tab.nprob), "s"(tab.p[1].tile_begin), "s"(tab.p[2].tile_begin),
-               "s"(tab.p[3].tile_begin));
   const int b = xcd_tile(nb);
   TL_MARK(0);
   if (b >= nb) return;
   int pi = 0;
-#pragma unroll
-  for (int i = 1; i < kMaxProbs; ++i)
-    if (i < tab.nprob && b >= tab.p[i].tile_begin) pi = i;
+  if (nprob > 1 && b >= tb1) pi = 1;
+  if (nprob > 2 && b >= tb2) pi = 2;
+  if (nprob > 3 && b >= tb3) pi = 3;
+  pi = __builtin_amdgcn_readfirstlane(pi);     // one scalar index (not a select per field address)
   const GemmProb& P = tab.p[pi];
-  // Every kernel-argument field this workgroup reads, requested in ONE scalar-load batch: left
-  // to itself the compiler requests each where first used, a chain of ~4 dependent kernarg
-  // round trips (~1.1 us) ahead of the first operand load (tools/tl_probe.py).
-  asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.W), "s"(P.ldw), "s"(P.Nout),
-               "s"(P.C), "s"(P.ldc), "s"(P.relu), "s"(P.tile_begin), "s"(P.bias), "s"(P.lng), "s"(P.lnb),
-               "s"(P.stats), "s"(P.Aout), "s"(P.ldao), "s"(P.H), "s"(P.ldh), "s"(P.norm), "s"(P.B));
+  // every field this workgroup reads, requested in ONE scalar-load batch: left to itself the
+  // compiler requests each where first used, a chain of dependent kernarg round trips ahead of
+  // the first operand load (tools/tl_probe.py)
+  asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.H), "s"(P.stats), "s"(P.Aout), "s"(P.W), "s"(P.bias),
+               "s"(P.C), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.ldh), "s"(P.ldao), "s"(P.ldw), "s"(P.Nout),
+               "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.hot_pad));
   if constexpr (PRO == kProGather)
     asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]),
                  "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
@@ -1318,7 +1322,10 @@ __global__ __launch_bounds__(256) void polyak_flat_kernel(float* T, const float*
 template <int MODE, int WN, int PRO>
 static void gl(const GemmTable& t, int nblocks, int Bp, int lds, Counters* bump, int ba, hipStream_t s) {
   const int padded = (nblocks + 7) & ~7;
-  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(64 * kNW), lds, s, t, Bp, bump, ba, nblocks);
+  const int tb1 = t.nprob > 1 ? t.p[1].tile_begin : nblocks, tb2 = t.nprob > 2 ? t.p[2].tile_begin : nblocks;
+  const int tb3 = t.nprob > 3 ? t.p[3].tile_begin : nblocks;
+  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(64 * kNW), lds, s, nblocks, t.nprob, tb1,
+                     tb2, tb3, Bp, t, bump, ba);
 }
 
 using GemmFn = void (*)(const GemmTable&, int, int, int, Counters*, int, hipStream_t);
