@@ -57,8 +57,10 @@ class Box:
         self.shape = tuple(shape)
 
 
-def stage_table(pol, rb, batch, iters=50):
-    """Per-stage mean device time (HIP events, handle stream) for an odd and an even step."""
+def stage_table(pol, rb, batch, iters=50, reps=5):
+    """Per-stage device time (HIP events, handle stream) for an odd and an even step: the median
+    over `reps` runs of the mean of iters/reps back-to-back launches (a host or clock hiccup in
+    one run does not move the figure)."""
     lib, h = pol._lib, pol._h
     rows = []
     ms = (C.c_float * 128)()
@@ -74,11 +76,14 @@ def stage_table(pol, rb, batch, iters=50):
             if names[i].endswith("_allreduce"):
                 continue          # a collective cannot be re-launched on its own
             t = C.c_float()
-            rc = lib.td3_time_stage(h, i, iters, C.byref(t))
-            if rc:
-                raise RuntimeError(lib.td3_last_error().decode())
+            runs = []
+            for _ in range(reps):
+                rc = lib.td3_time_stage(h, i, max(1, iters // reps), C.byref(t))
+                if rc:
+                    raise RuntimeError(lib.td3_last_error().decode())
+                runs.append(float(t.value))
             rows.append(dict(phase=phase, stage=names[i], kernel=kernels[i],
-                             ms=float(t.value), flops=float(flops[i])))
+                             ms=float(np.median(runs)), flops=float(flops[i])))
     return rows
 
 
@@ -237,7 +242,8 @@ def main():
 
     rows, fam, roof = None, None, None
     if not args.no_roofline:           # every rank runs it: profiled steps contain collectives
-        rows = stage_table(pol, rb, B, iters=50 if cfg["kind"] != "particles" else 3)
+        rows = stage_table(pol, rb, B, iters=50 if cfg["kind"] != "particles" else 3,
+                           reps=5 if cfg["kind"] != "particles" else 1)
         if rank == 0:
             pmc = None
             pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -443,20 +443,44 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4[o][jj];
     }
-  for (int o = kHeadRegs; o < ad; ++o) {                              // wide action spaces
-    float w1o[8], w4o[8];
+  // wide action spaces (Humanoid: 17): further blocks of kHeadRegs outputs, each block's W1
+  // columns and W4 rows requested in one batch (one load round trip per block, not per output)
+  for (int ob = kHeadRegs; ob < ad; ob += kHeadRegs) {
+    float w1b[kHeadRegs][8], w4b[kHeadRegs][8];
+    const int s0 = sd + ob, sa = s0 & ~3, so = s0 & 3;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const int n = rcol(c.lane, jj);
-      w1o[jj] = n < K0 ? gld(P.ex[4] + ((size_t)n * ldw1 + sd + o)) : 0.f;
-    }
-    rv_load(w4o, P.ex[6] + (size_t)o * ldw4, ldw4, c.lane);
-    const float ga = wsum(rv_pdot(gu0[0], w1o, K0, c.lane));
-    const float t = gld(P.ex[5] + ((size_t)c.row * 32 + o));
-    const float gz4 = live ? (ga * ma) * (1.f - t * t) : 0.f;
-    if (c.lane == 0) gst(P.ex[10] + ((size_t)c.row * 32 + o), gz4);
+      const float* wp = P.ex[4] + ((size_t)rcol(c.lane, jj) * ldw1 + sa);
+      float v[12];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4o[jj];
+      for (int q = 0; q < 3; ++q) {
+        const float4 t = gld4(wp + 4 * q);
+        v[4 * q + 0] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      }
+#pragma unroll
+      for (int o = 0; o < kHeadRegs; ++o) {
+        const float x = so == 0 ? v[o] : so == 1 ? v[o + 1] : so == 2 ? v[o + 2] : v[o + 3];
+        w1b[o][jj] = ob + o < ad ? x : 0.f;
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < kHeadRegs; ++o) {
+      const int oo = ob + o < ad ? ob + o : 0;
+      rv_load(w4b[o], P.ex[6] + (size_t)oo * ldw4, ldw4, c.lane);
+    }
+    float pb[kHeadRegs];
+#pragma unroll
+    for (int o = 0; o < kHeadRegs; ++o) pb[o] = rv_pdot(gu0[0], w1b[o], K0, c.lane);
+#pragma unroll
+    for (int o = 0; o < kHeadRegs; ++o)
+      if (ob + o < ad) {
+        const float ga = wsum(pb[o]);
+        const float t = __shfl(tl, ob + o, 64);
+        const float gz4 = live ? (ga * ma) * (1.f - t * t) : 0.f;
+        if (c.lane == 0) gst(P.ex[10] + ((size_t)c.row * 32 + ob + o), gz4);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4b[o][jj];
+      }
   }
   rv_store(P.ex[11] + (size_t)c.row * ld3, ld3, c.lane, gu3[0]);
   ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, NORM);        // dZ3 of the actor
@@ -1224,9 +1248,9 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   const int t = b - P.tile_begin;
   const int ntn = (P.Np + 63) >> 6;
   const int nmat = ntn * P.ntk;                      // ntk = k tiles of 64 in this mode
-  const AdamK k = make_adam(a.adam);
+  const AdamPw pw = adam_pw(a.adam);
   if (t >= nmat) {
-    dw_vector_tile_cols<512>(a, P, k, t - nmat, sm);
+    dw_vector_tile_cols<512>(a, P, make_adam(a.adam, pw), t - nmat, sm);
     return;
   }
   const int kt = t % P.ntk, nt = t / P.ntk;
@@ -1288,6 +1312,9 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
     for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[r];
   }
   __syncthreads();
+  // (the optimizer state is requested here, not behind the first operand steps: there its 64
+  // loads per lane sat in front of the later steps' operand loads in the in-order vmcnt queue,
+  // Humanoid C_dw 49 -> 60 us)
   if (rh == 0) {
     const int kk = k0 + qk * 32 + i;
     int64_t idx[16];
@@ -1300,7 +1327,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
       ok[r] = n < P.Np && kk < P.Kp;
       idx[r] = P.offW + (int64_t)n * P.Kp + kk;
     }
-    apply_grads<16>(a, k, idx, gq, ok);
+    apply_grads<16>(a, make_adam(a.adam, pw), idx, gq, ok);
   }
 }
 
