@@ -25,7 +25,15 @@ enum Pro : int {
   kProLNBwd = 2,       // dZ = relu'(LN_bwd(dU)) of the following layer
   kProGather = 3,      // replay-ring rows of this step: Philox index draw + record read (the
                        // sample() of my_replay_buffer.py:119-128 fused into the first layer)
+  kProL0 = 4,          // layer 0 (input width <= 32) recomputed for the workgroup's 32 rows on
+                       // MFMA, ReLU, LayerNorm: the A rows of layer 1 (one launch for two layers)
+  kProL0G = 5,         // kProL0 with the input rows sampled from the replay ring (as kProGather)
 };
+// kProL0 / kProL0G operand slots: ex[8] = W0 [N0p][32], ex[9] = b0, ex[10] = H0 out (nullable,
+// ld exi[5]), exi[5] = N0p (<= 512, the layer-1 Kp), exi[6] = K0 (input width, <= 32),
+// kProL0G ring outputs: ex[3] (ld exi[8]) and ex[0] (ld exi[3]) = copies of the input row,
+// ex[1] / ex[2] = reward / not_done (record offset exi[1]); exi[0] = record offset of the input.
+constexpr int kL0XS = 36;        // LDS row stride of the staged layer-0 input rows
 
 // Row kernels (one batch row per wave) between the GEMM stages; they reuse GemmProb's
 // ex / exi / exf operand slots (layout documented at each row function in kernels.hip).

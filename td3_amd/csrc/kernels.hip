@@ -200,6 +200,134 @@ __device__ __forceinline__ void pro_gather(const GemmProb& P, const RingSide& rs
   }
 }
 
+// ---- kProL0 / kProL0G: layer 0 inside the layer-1 launch --------------------------------
+// Stage 1: the workgroup's 32 input rows (<= 32 wide) into LDS xs[32][kL0XS], each wave its
+// kRPW rows (lane half h = row parity, lane i = column).  l0_load_x requests them FIRST in the
+// kernel (ahead of the weights: vmcnt retires in order); kProL0G draws them from the ring exactly
+// as pro_gather.  l0_put_x writes them to LDS and, in n-tile 0, stores the copies / reward /
+// not_done / drawn rows.
+constexpr int kL0R = kRPW / 2;
+struct L0X {
+  float x[kL0R], rw[kL0R];
+  int64_t idx[kL0R];
+};
+template <bool GATHER>
+__device__ __forceinline__ void l0_load_x(const GemmProb& P, const RingSide& rs, const Ctx& c, L0X& X) {
+  const int K0 = P.exi[6];
+  const int i = c.lane & 31, h = c.lane >> 5;
+  const bool t0 = c.nt == 0;
+  uint64_t step = 0, n = 0;
+  if constexpr (GATHER) {
+    step = (uint64_t)(rs.ctr->total_it + 1);
+    n = (uint64_t)*rs.d_size;
+  }
+  const int col = i;
+  const bool valid = i < K0;
+#pragma unroll
+  for (int rr = 0; rr < kL0R; ++rr) {
+    const int row = c.wave * kRPW + 2 * rr + h, grow = c.m0 + row;
+    X.x[rr] = 0.f;
+    X.rw[rr] = 0.f;
+    if constexpr (GATHER) {
+      const int64_t idx = grow < P.B ? (int64_t)philox_index(rs.seed, step, (uint32_t)grow, n) : -1;
+      X.idx[rr] = idx;
+      if (idx >= 0) {
+        const float* rec = rs.data + (size_t)idx * rs.rec;
+        if (valid) X.x[rr] = gld(rec + P.exi[0] + col);
+        if (t0 && i < 2 && P.ex[1 + i]) X.rw[rr] = gld(rec + P.exi[1] + i);
+      }
+    } else {
+      X.x[rr] = gld(P.A + (size_t)grow * P.lda + col);  // input rows are >= 32 wide (zero pads)
+    }
+  }
+}
+
+template <bool GATHER>
+__device__ __forceinline__ void l0_put_x(const GemmProb& P, const RingSide& rs, float* xs, const Ctx& c, int pi,
+                                         const L0X& X) {
+  const int K0 = P.exi[6];
+  const int i = c.lane & 31, h = c.lane >> 5;
+  const bool t0 = c.nt == 0;
+  const int col = i;
+  const bool valid = i < K0;
+#pragma unroll
+  for (int rr = 0; rr < kL0R; ++rr) {
+    const int row = c.wave * kRPW + 2 * rr + h, grow = c.m0 + row;
+    xs[row * kL0XS + i] = X.x[rr];
+    if constexpr (GATHER) {
+      if (t0) {
+        if (valid) {
+          if (P.ex[3]) gst(P.ex[3] + (size_t)grow * P.exi[8] + col, X.x[rr]);
+          if (P.ex[0]) gst(P.ex[0] + (size_t)grow * P.exi[3] + col, X.x[rr]);
+        }
+        if (i < 2 && P.ex[1 + i]) gst(P.ex[1 + i] + grow, X.rw[rr]);
+        if (pi == 0 && rs.idx_out && i == 0 && grow < P.B) rs.idx_out[grow] = X.idx[rr];
+      }
+    }
+  }
+}
+
+// Stage 2: Z0 = X * W0^T on MFMA (wave w: layer-0 column tiles w and w + 8), + b0, ReLU, into the
+// layer-1 A buffer (LDS, [32][S]); n-tile 0 also stores H0 (the backward's post-ReLU rows).
+// (Halving the MFMAs by laying the K0 <= 24 inputs out as k = 12h + s cost more in operand
+// shuffles than the 4 MFMAs per tile it saved: TF_fwd01 12.3 -> 12.4-14 us.)
+__device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, float* smem, const Ctx& c,
+                                        const float (&w0)[2][16], const float (&b0)[2]) {
+  const int i = c.lane & 31, h = c.lane >> 5;
+  const int n0t = P.exi[5] >> 5;
+  const float* arow = xs + i * kL0XS + 16 * h;
+  float av[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(arow + 4 * q);
+    av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
+  }
+  float* H0 = P.ex[10];
+  const bool t0 = c.nt == 0;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int tile = c.wave + kNW * ct;
+    if (tile >= n0t) continue;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], w0[ct][s], acc);
+    const int col = tile * 32 + i;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = mfma_row(r, c.lane);
+      const float v = fmaxf(acc[r] + b0[ct], 0.f);
+      smem[row * c.S + col] = v;
+      if (t0 && H0) gst(H0 + (size_t)(c.m0 + row) * P.exi[5] + col, v);
+    }
+  }
+}
+
+// Stage 3: LayerNorm 0 of the A buffer rows in place (each wave its kRPW rows); n-tile 0 stores
+// U0 (Aout) and the row statistics, as pro_ln.
+__device__ __forceinline__ void l0_ln(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = kRPW;
+  float x[RB][8], g[8], bb[8], mean[RB], rstd[RB], rm[8];
+  rv_load(g, P.lng, P.Kp, c.lane);
+  rv_load(bb, P.lnb, P.Kp, c.lane);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rv_load_lds(x[r], smem + (c.wave * kRPW + r) * c.S, P.Kp, c.lane);
+  real_mask(rm, P.Kreal, c.lane);
+  ln_fwd_rows_pk<RB>(x, g, bb, rm, 1.0f / (float)P.Kreal, mean, rstd);
+  const bool t0 = c.nt == 0;
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int row = c.wave * kRPW + r, grow = c.m0 + row;
+    lds_put_row(smem, c.S, row, P.Kp, c.lane, x[r]);
+    if (t0 && P.Aout) rv_store(P.Aout + (size_t)grow * P.ldao, P.Kp, c.lane, x[r]);
+    if (t0 && P.stats && c.lane == 0) {
+      gst(P.stats + (grow), mean[r]);
+      gst(P.stats + (c.Bp + grow), rstd[r]);
+    }
+  }
+}
+
 // ================================================================== row kernels
 // One batch row per wave (grid: Bp/4 x nprob, 256 threads): the head / loss work between the
 // GEMM stages.  Every operand of the row (and the head weights) is requested up front, the
@@ -738,10 +866,14 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(int nb, int nprob, int t
   asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.H), "s"(P.stats), "s"(P.Aout), "s"(P.W), "s"(P.bias),
                "s"(P.C), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.ldh), "s"(P.ldao), "s"(P.ldw), "s"(P.Nout),
                "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.hot_pad));
-  if constexpr (PRO == kProGather)
+  constexpr bool kL0 = PRO == kProL0 || PRO == kProL0G;
+  if constexpr (PRO == kProGather || PRO == kProL0G)
     asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]),
                  "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
                  "s"(tab.rs.ctr));
+  if constexpr (kL0)
+    asm volatile("" ::"s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.ex[3]),
+                 "s"(P.exi[8]));
   const int mtiles = Bp >> 5;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
@@ -765,10 +897,30 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(int nb, int nprob, int t
   // bias of the epilogue's column, requested with the weights (off the tail of the chain)
   const int bcol = (WK == 1) ? ncol : n0 + (int)(threadIdx.x % OUTW);
   const float bias = (MODE == 0 && P.bias && (WK > 1 ? bcol < P.Nout : active)) ? gld(P.bias + bcol) : 0.f;
+  const Ctx c{m0, wave, lane, nt, Bp, S};
+  // kProL0*: the input rows first, then the wave's layer-0 weight tiles (B operand:
+  // W0[tile*32 + i][16h .. 16h+15]) and biases, then the layer-1 weights
+  L0X l0x;
+  if constexpr (kL0) l0_load_x<PRO == kProL0G>(P, tab.rs, c, l0x);
+  float w0[2][16], b0v[2];
+  if constexpr (kL0) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int tile = min(wave + kNW * ct, (P.exi[5] >> 5) - 1);
+      const float* wp = P.ex[8] + (size_t)(tile * 32 + i) * 32 + 16 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = gld4(wp + 4 * q);
+        w0[ct][4 * q + 0] = v.x; w0[ct][4 * q + 1] = v.y; w0[ct][4 * q + 2] = v.z; w0[ct][4 * q + 3] = v.w;
+      }
+      b0v[ct] = gld(P.ex[9] + tile * 32 + i);
+    }
+  }
   if constexpr (kPrefetchB) {
     load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
   }
+
   TL_MARK(5);
   // WN >= 2 waves own more chunks than kCh: the next two are requested right behind the A rows
   // (in flight during the LayerNorm, not queued ahead of it), the rest stream in the MFMA loop
@@ -781,14 +933,26 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(int nb, int nprob, int t
     }
   };
 
-  const Ctx c{m0, wave, lane, nt, Bp, S};
   if constexpr (PRO == kProCopy) pro_copy<kRPW>(P, smem, c);
   else if constexpr (PRO == kProLN) pro_ln(P, smem, c, issue_stream);
   else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
   else if constexpr (PRO == kProGather) pro_gather(P, tab.rs, smem, c, pi);
+  else if constexpr (kL0) {
+    float* xs = smem + 32 * S;
+    l0_put_x<PRO == kProL0G>(P, tab.rs, xs, c, pi, l0x);
+    __syncthreads();
+    TL_MARK(6);
+    l0_mfma(P, xs, smem, c, w0, b0v);
+    if (P.norm) {
+      __syncthreads();
+      TL_MARK(7);
+      l0_ln(P, smem, c);
+    }
+    issue_stream();
+  }
   __syncthreads();
   TL_MARK(1);
-  if constexpr (PRO != kProLN) issue_stream();
+  if constexpr (PRO != kProLN && !kL0) issue_stream();
 
   f32x16 acc;
 #pragma unroll
@@ -1365,6 +1529,8 @@ static GemmFn pick_fwd(int pro) {
     case kProCopy: return gl<0, WN, kProCopy>;
     case kProLN: return gl<0, WN, kProLN>;
     case kProGather: return gl<0, WN, kProGather>;
+    case kProL0: return gl<0, WN, kProL0>;
+    case kProL0G: return gl<0, WN, kProL0G>;
   }
   return nullptr;
 }
@@ -1481,6 +1647,8 @@ static int set_attr_all() {
   TD3_ATTR(0, kProCopy);
   TD3_ATTR(0, kProLN);
   TD3_ATTR(0, kProGather);
+  TD3_ATTR(0, kProL0);
+  TD3_ATTR(0, kProL0G);
   TD3_ATTR(1, kProCopy);
   TD3_ATTR(1, kProLNBwd);
 #undef TD3_ATTR

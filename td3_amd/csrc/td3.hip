@@ -367,12 +367,24 @@ static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd) {
 
 // Forward layers 0..2 of several networks (one launch per layer); layer 0 copies the
 // network input rows, layers 1 and 2 apply the previous layer's LayerNorm in the prologue.
+// fuse_l0: layer 0 is recomputed inside the layer-1 launch (kProL0 / kProL0G) when every network's
+// input is <= 32 wide (HalfCheetah, Pendulum): one dependent launch fewer per forward chain.
+static bool can_fuse_l0(const std::vector<FwdItem>& items) {
+  for (auto& it : items) {
+    const NetL& n = *it.net;
+    if (n.lnin || n.D > 0 || n.lin[0].Kp != 32 || n.lin[0].Np > 512 || n.lin[1].Kp != n.lin[0].Np) return false;
+    if (it.ring_src < 0 && (it.e->ldx < 32)) return false;
+  }
+  return true;
+}
+
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
                           Counters* bump, int bump_actor, const RingSide* ring = nullptr,
-                          const RingOut* ro = nullptr, int o_r = 0) {
+                          const RingOut* ro = nullptr, int o_r = 0, bool fuse_l0 = false) {
   const bool norm = h->cfg.norm != 0;
-  for (int l = 0; l < 3; ++l) {
+  fuse_l0 = fuse_l0 && can_fuse_l0(items);
+  for (int l = fuse_l0 ? 1 : 0; l < 3; ++l) {
     std::vector<GemmProb> probs;
     int maxKp = 0;
     int wn1_blocks = 0;
@@ -382,8 +394,10 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     }
     const int wn = gemm_wn(maxKp, Bp, wn1_blocks, true);
     const bool lnin = items[0].net->lnin;          // TD3_particles lnorm1 on the MLP input
-    const bool gather = ring && l == 0;
-    const int pro = gather ? kProGather : l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
+    const bool l0 = fuse_l0 && l == 1;             // this launch also computes layer 0
+    const bool gather = ring && (l == 0 || l0);
+    int pro = gather ? kProGather : l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
+    if (l0) pro = gather ? kProL0G : kProL0;
     int blocks = 0, lds = 0;
     double flops = 0;
     for (size_t k = 0; k < items.size(); ++k) {
@@ -417,7 +431,7 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
           }
         }
       }
-      if (gather) {
+      if (gather && !l0) {
         TD3_ARG(it.ring_src >= 0 && !lnin && ro, "internal: ring-sampled layer without a record field");
         p.exi[0] = it.ring_src;
         p.Aout = ro[k].a;
@@ -427,6 +441,29 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
         p.ex[1] = ro[k].r;
         p.ex[2] = ro[k].nd;
         p.exi[1] = o_r;
+      }
+      if (l0) {                                   // layer-0 operands (kernels.h kProL0 slots)
+        const LinearL& L0 = it.net->lin[0];
+        if (!gather) {
+          p.A = it.e->X;
+          p.lda = it.e->ldx;
+        }
+        p.ex[8] = const_cast<float*>(it.P + L0.offW);
+        p.ex[9] = const_cast<float*>(it.P + L0.offb);
+        p.ex[10] = (it.stats || (!norm && it.store_u)) ? it.e->H[0] : nullptr;
+        p.exi[5] = L0.Np;
+        p.exi[6] = L0.K;
+        if (gather) {
+          TD3_ARG(it.ring_src >= 0 && ro, "internal: ring-sampled layer without a record field");
+          p.exi[0] = it.ring_src;
+          p.ex[3] = ro[k].a;
+          p.exi[8] = ro[k].lda;
+          p.ex[0] = ro[k].b;
+          p.exi[3] = ro[k].ldb;
+          p.ex[1] = ro[k].r;
+          p.ex[2] = ro[k].nd;
+          p.exi[1] = o_r;
+        }
       }
       p.Kreal = L.K;
       p.Kp = L.Kp;
@@ -441,12 +478,15 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.tile_begin = blocks;
       blocks += (Bp / 32) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
-      lds = std::max(lds, gemm_lds_bytes(L.Kp));
+      lds = std::max(lds, gemm_lds_bytes(L.Kp) + (l0 ? 32 * kL0XS * 4 : 0));
+      if (l0) flops += 2.0 * Bp * it.net->lin[0].N * it.net->lin[0].K;
       probs.push_back(p);
     }
+    // the step counters are bumped by the launch after the one that draws the sample
+    const int bump_l = fuse_l0 ? 2 : 1;
     TD3_RC(push_gemm_stage(h, owned, st, probs, 0, wn, pro, Bp, lds, blocks, flops,
-                           std::string(tag) + "_fwd" + std::to_string(l), l == 1 ? bump : nullptr,
-                           bump_actor, gather ? ring : nullptr));
+                           std::string(tag) + (l0 ? "_fwd01" : "_fwd" + std::to_string(l)),
+                           l == bump_l ? bump : nullptr, bump_actor, gather ? ring : nullptr));
   }
   return 0;
 }
@@ -786,7 +826,7 @@ static int build_step(td3_handle* h, int B) {
       std::vector<FwdItem> f1 = {{&an, Pta, &P->TA, false, false}, {&q1, Pq1, &P->Q[0], true, true},
                                  {&q2, Pq2, &P->Q[1], true, true}};
       if (actor_phase) f1.push_back({&an, Pa, &P->A, true, true});
-      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase));
+      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase, nullptr, nullptr, 0, true));
       {  // the ring-sampled first layer (record layout [s | a | s' | r | not_done], replay.hip)
         // the first column tile of each problem keeps what the later stages read: the target-twin
         // input s' (X_S2A), the twin dW input [s | a] (X_SA), reward / not_done, and on policy
@@ -802,7 +842,7 @@ static int build_step(td3_handle* h, int B) {
                          {nullptr, 0, nullptr, 0, P->R, P->ND},
                          {P->X_S, P->ld_s, P->X_SP, P->ld_sa, nullptr, nullptr}};
         TD3_RC(add_fwd_stages(h, P->tables, fr, f1r, Bp, B, "F", h->d_ctr, actor_phase, &P->rside, ro,
-                              2 * sd + ad));
+                              2 * sd + ad, true));
         P->body_ring[actor_phase][inj].push_back(fr[0]);
       }
       // ---- heads: a' = target smoothing into X_S2A (:131-137); pi(s) into X_SP (:159)
@@ -813,7 +853,7 @@ static int build_step(td3_handle* h, int B) {
       }
       // ---- target twin on (s', a')
       std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
-      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0));
+      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, nullptr, nullptr, 0, true));
       // ---- critic loss (clipped double-Q target, mse) and LN3 backward of the twin
       {
         std::vector<GemmProb> cl;
@@ -863,7 +903,7 @@ static int build_step(td3_handle* h, int B) {
       if (!actor_phase) continue;
       // ---------------- delayed policy update (TD3_featured.py:156-171)
       std::vector<FwdItem> f3 = {{&q1, Pq1, &P->AQ, false, true}};
-      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0));
+      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0, nullptr, nullptr, 0, true));
       {
         GemmProb p{};
         p.norm = norm ? 1 : 0;

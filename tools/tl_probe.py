@@ -76,9 +76,9 @@ def main():
             t5, t6, t7 = v[:, 5], v[:, 6], v[:, 7]
             fine = f"   mark5 {np.median(t5 - t0) * 0.01:5.2f}"
             if t6.min() > 0:
-                fine += f" rows_in {np.median(t6 - t0) * 0.01:5.2f} ln_done {np.median(t7 - t0) * 0.01:5.2f}"
+                fine += f" mark6 {np.median(t6 - t0) * 0.01:5.2f} mark7 {np.median(t7 - t0) * 0.01:5.2f}"
             print(fine)
-            if name in ("F_fwd1", "TF_fwd1", "C_dw") and phase == 1:
+            if name in ("F_fwd1", "F_fwd01", "TF_fwd1", "TF_fwd01", "C_dw") and phase == 1:
                 xcc = v[:, 4]
                 print("   per-XCC wg counts:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
                 q = np.percentile((t1 - t0) * 0.01, [10, 50, 90])
