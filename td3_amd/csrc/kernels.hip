@@ -843,7 +843,7 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 // the problem select costs no memory round trip; the problem's fields are then the first and only
 // kernel-argument round trip ahead of the operand loads.
 template <int MODE, int WN, int PRO>
-__global__ __launch_bounds__(64 * kNW) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
+__global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
                                                         GemmTable tab, Counters* bump, int bump_actor) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
@@ -926,8 +926,10 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(int nb, int nprob, int t
   // (in flight during the LayerNorm, not queued ahead of it), the rest stream in the MFMA loop
   float bs0[16], bs1[16];
   const int s0 = cb + kCh;
+  // WN = 4 (B >= 512, two workgroups per CU at <= 128 VGPRs) requests them after the prologue:
+  // in flight during the LayerNorm they pushed the kernel past 128 VGPRs
   auto issue_stream = [&]() {
-    if constexpr (WN >= 2) {
+    if constexpr (WN == 2) {
       if (s0 < ce) load_chunk<MODE>(P, bs0, s0, ncol, h);
       if (s0 + 1 < ce) load_chunk<MODE>(P, bs1, s0 + 1, ncol, h);
     }
@@ -953,6 +955,10 @@ __global__ __launch_bounds__(64 * kNW) void gemm_kernel(int nb, int nprob, int t
   __syncthreads();
   TL_MARK(1);
   if constexpr (PRO != kProLN && !kL0) issue_stream();
+  if constexpr (WN == 4) {
+    if (s0 < ce) load_chunk<MODE>(P, bs0, s0, ncol, h);
+    if (s0 + 1 < ce) load_chunk<MODE>(P, bs1, s0 + 1, ncol, h);
+  }
 
   f32x16 acc;
 #pragma unroll
