@@ -79,8 +79,14 @@ def main():
                 fine += f" mark6 {np.median(t6 - t0) * 0.01:5.2f} mark7 {np.median(t7 - t0) * 0.01:5.2f}"
             print(fine)
             if name in ("F_fwd1", "F_fwd01", "TF_fwd1", "TF_fwd01", "C_dw") and phase == 1:
-                xcc = v[:, 4]
+                xcc = v[:, 4] & 0xFFFFFFFF
+                hw = v[:, 4] >> 32
                 print("   per-XCC wg counts:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
+                # HW_ID: wave id [3:0], simd [5:4], pipe [7:6], cu [11:8], sh [12], se [15:13]
+                cu = (xcc << 16) | (hw & 0xFF00)
+                _, cnt = np.unique(cu, return_counts=True)
+                print("   workgroups per CU (histogram 1,2,3..):", np.bincount(cnt).tolist()[1:],
+                      " distinct CUs:", len(cnt))
                 q = np.percentile((t1 - t0) * 0.01, [10, 50, 90])
                 print("   end p10/50/90/max:", np.round(np.percentile((t3 - base) * 0.01, [10, 50, 90, 100]), 2).tolist(),
                       " dur p10/50/90/max:", np.round(np.percentile((t3 - t0) * 0.01, [10, 50, 90, 100]), 2).tolist())
