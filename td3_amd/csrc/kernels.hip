@@ -40,9 +40,10 @@ __device__ __forceinline__ void tl_mark(int k) {
     if (k == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     td3_tl[id][k] = __builtin_amdgcn_s_memrealtime();
     if (k == 0) {
-      unsigned x;
+      unsigned x, hw;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-      td3_tl[id][4] = x;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      td3_tl[id][4] = x | ((unsigned long long)hw << 32);
     }
   }
 }
