@@ -360,9 +360,12 @@ static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<
 //     13.8 us, F_fwd2 13.9 -> 12.4 us; WN=4 there is slower (18.3 us), and the input-grad
 //     stages (strided weight reads) lose with WN=2 (CB_bwd1 9.0 -> 10.8 us).
 // Narrow K (<= 128) always uses WN=4.
+#ifndef TD3_WN2_MIN
+#define TD3_WN2_MIN 256
+#endif
 static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd) {
   if (maxK <= 128 || (Bp >= 512 && wn1_blocks >= 256)) return 4;
-  return (fwd && wn1_blocks >= 256) ? 2 : 1;
+  return (fwd && wn1_blocks >= TD3_WN2_MIN) ? 2 : 1;
 }
 
 // Forward layers 0..2 of several networks (one launch per layer); layer 0 copies the
