@@ -186,8 +186,9 @@ int td3_profile_stages(td3_handle* h, rb_handle* rb, int batch, int actor_phase,
 const char* td3_stage_name(td3_handle* h, int i);
 /* HIP kernel function launched by stage i (the name rocprofv3 reports). */
 const char* td3_stage_kernel(td3_handle* h, int i);
-/* Re-launch one stage `iters` times back-to-back between two HIP events on the
- * handle stream (after one full step at `batch`); returns mean ms per launch. */
+/* Re-launch one stage `iters` times back-to-back (captured in one hipGraph, replayed between
+ * two HIP events on the handle stream, after one full step at `batch`); returns mean ms per
+ * launch. */
 int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean);
 /* Algorithmic FLOPs of one launch of stage i (MFMA stages; 0 otherwise). */
 double td3_stage_flops(td3_handle* h, int i);

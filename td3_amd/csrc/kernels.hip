@@ -501,6 +501,26 @@ __device__ __forceinline__ void row_actor_loss(const GemmProb& P, const RowCtx& 
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
 }
 
+// W[:, s0 .. s0+kHeadRegs): those columns of the 8 W rows a lane owns (rcol), as two float4 loads
+// per row at the (4-B aligned) column s0 itself; columns at or past `lim` are 0.  (Aligned loads
+// from below s0 needed a select on the uniform offset, which compiled to branches with a full
+// load drain per row: 8 dependent load round trips.)
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void head_cols(const float* W, int ldw, int s0, int lim, int lane,
+                                          float (&out)[kHeadRegs][8]) {
+  static_assert(kHeadRegs == 8, "two float4 per row");
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const float* wp = W + ((size_t)rcol(lane, jj) * ldw + s0);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const f32x4u t = *reinterpret_cast<const f32x4u*>(wp + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[4 * q + e][jj] = 4 * q + e < lim ? t[e] : 0.f;
+    }
+  }
+}
+
 // ---- dQ1/da through Q1's first layer, then the actor's head and LN3 backward -------------
 // ex[0]=dU0 of Q1(s,pi) ex[1]=H0 of Q1(s,pi) ex[2]=stats0 ex[3]=gamma0(q1) ex[4]=W1(q1)
 // ex[5]=T (tanh out) ex[6]=W4(actor) ex[7]=H3(actor) ex[8]=stats3(actor) ex[9]=gamma3(actor)
@@ -529,26 +549,7 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
     rs0[0] = rs3[0] = 1.f;
   }
   const float tl = c.lane < ad ? gld(P.ex[5] + ((size_t)c.row * 32 + c.lane)) : 0.f;
-  // W1[:, sd+o]: the action columns of each W1 row the lane needs, as three float4 loads
-  // from the 16-B aligned column below sd (rows are contiguous; pads are zero)
-  {
-    const int sa = sd & ~3, so = sd & 3;
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const float* wp = P.ex[4] + ((size_t)rcol(c.lane, jj) * ldw1 + sa);
-      float v[12];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const float4 t = gld4(wp + 4 * q);
-        v[4 * q + 0] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
-      }
-#pragma unroll
-      for (int o = 0; o < kHeadRegs; ++o) {
-        const float x = so == 0 ? v[o] : so == 1 ? v[o + 1] : so == 2 ? v[o + 2] : v[o + 3];
-        w1[o][jj] = o < ad ? x : 0.f;
-      }
-    }
-  }
+  head_cols(P.ex[4], ldw1, sd, ad, c.lane, w1);        // W1[:, sd+o]: the action columns
 #pragma unroll
   for (int o = 0; o < kHeadRegs; ++o) {
     const int oo = o < ad ? o : 0;
@@ -576,22 +577,7 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
   // columns and W4 rows requested in one batch (one load round trip per block, not per output)
   for (int ob = kHeadRegs; ob < ad; ob += kHeadRegs) {
     float w1b[kHeadRegs][8], w4b[kHeadRegs][8];
-    const int s0 = sd + ob, sa = s0 & ~3, so = s0 & 3;
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const float* wp = P.ex[4] + ((size_t)rcol(c.lane, jj) * ldw1 + sa);
-      float v[12];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const float4 t = gld4(wp + 4 * q);
-        v[4 * q + 0] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
-      }
-#pragma unroll
-      for (int o = 0; o < kHeadRegs; ++o) {
-        const float x = so == 0 ? v[o] : so == 1 ? v[o + 1] : so == 2 ? v[o + 2] : v[o + 3];
-        w1b[o][jj] = ob + o < ad ? x : 0.f;
-      }
-    }
+    head_cols(P.ex[4], ldw1, sd + ob, ad - ob, c.lane, w1b);
 #pragma unroll
     for (int o = 0; o < kHeadRegs; ++o) {
       const int oo = ob + o < ad ? ob + o : 0;
