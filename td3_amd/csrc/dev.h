@@ -46,13 +46,30 @@ __device__ __forceinline__ void gst(float* p, float v) { *(GAS float*)p = v; }
 // A lane's slice of a row of width <= 512: v[4q+e] = row[lane*4 + 256q + e].
 __device__ __forceinline__ int rcol(int lane, int j) { return lane * 4 + ((j >> 2) << 8) + (j & 3); }
 
+// Lanes past n keep zeros by an exec-masked load (no select on the loaded value: such selects,
+// interleaved by the scheduler with later loads, put load drains between a row's requests).
 __device__ __forceinline__ void rv_load(float (&v)[8], const float* __restrict__ row, int n, int lane) {
   const int c0 = lane * 4, c1 = c0 + 256;
-  const float4 a = gld4(row + (c0 < n ? c0 : 0));
-  const float4 b = gld4(row + (c1 < n ? c1 : 0));
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (c0 < n) a = gld4(row + c0);
+  if (c1 < n) b = gld4(row + c1);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// rv_load in two halves, for callers that request many rows before the first use: the raw
+// float4 pair (clamped address), then the masked values (a scheduler free to interleave the
+// masks with later rows' loads puts partial load drains between them)
+__device__ __forceinline__ void rv_load_raw(float4 (&q)[2], const float* __restrict__ row, int n, int lane) {
+  const int c0 = lane * 4, c1 = c0 + 256;
+  q[0] = gld4(row + (c0 < n ? c0 : 0));
+  q[1] = gld4(row + (c1 < n ? c1 : 0));
+}
+__device__ __forceinline__ void rv_from_raw(float (&v)[8], const float4 (&q)[2], int n, int lane) {
+  const int c0 = lane * 4, c1 = c0 + 256;
   const bool va = c0 < n, vb = c1 < n;
-  v[0] = va ? a.x : 0.f; v[1] = va ? a.y : 0.f; v[2] = va ? a.z : 0.f; v[3] = va ? a.w : 0.f;
-  v[4] = vb ? b.x : 0.f; v[5] = vb ? b.y : 0.f; v[6] = vb ? b.z : 0.f; v[7] = vb ? b.w : 0.f;
+  v[0] = va ? q[0].x : 0.f; v[1] = va ? q[0].y : 0.f; v[2] = va ? q[0].z : 0.f; v[3] = va ? q[0].w : 0.f;
+  v[4] = vb ? q[1].x : 0.f; v[5] = vb ? q[1].y : 0.f; v[6] = vb ? q[1].z : 0.f; v[7] = vb ? q[1].w : 0.f;
 }
 
 __device__ __forceinline__ void rv_store(float* __restrict__ row, int n, int lane, const float (&v)[8]) {

@@ -130,6 +130,10 @@ struct LnBwdProb {
   const float* GU; const float* H; const float* stats; const float* lng; int ld, K;
   float* GZ;
 };
+constexpr int kMaxLnBwd = 3;
+struct LnBwdTable {            // by value in the kernel arguments (one scalar-load batch)
+  LnBwdProb p[kMaxLnBwd];
+};
 
 // ------------------------------------------------------------------ parameter-grad + Adam
 struct DwProb {
@@ -168,7 +172,7 @@ int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int 
                 Counters* bump, int bump_actor, hipStream_t s);
 int launch_rows(int kind, const GemmTable& t, int Bp, hipStream_t s);
 int launch_heads(const HeadArgs& a, int nprob, hipStream_t s);
-int launch_lnbwd_rows(const LnBwdProb* d_probs, int nprob, int Bp, int norm, hipStream_t s);
+int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s);
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s);
 int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s);
 int launch_polyak_flat(float* T, const float* P, int64_t n, float tau, hipStream_t s);

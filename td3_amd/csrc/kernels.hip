@@ -529,6 +529,12 @@ __device__ __forceinline__ void head_cols(const float* W, int ldw, int s0, int l
 // exf[0]=max_action
 template <bool NORM>
 __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowCtx& c) {
+  // every field in one scalar-load batch (left alone, the compiler requested them where used, in
+  // dependent kernel-argument round trips between the row's loads)
+  asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]),
+               "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.ex[11]),
+               "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[2]), "s"(P.exi[3]), "s"(P.exi[4]), "s"(P.exi[5]),
+               "s"(P.exi[6]), "s"(P.exi[7]), "s"(P.exf[0]), "s"(P.Aout), "s"(P.ldao), "s"(P.B));
   const int K0 = P.exi[0], ld0 = P.exi[1], ldw1 = P.exi[2], sd = P.exi[3], ad = P.exi[4];
   const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
   const float ma = P.exf[0];
@@ -762,7 +768,7 @@ __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const Ro
 }
 
 template <int KIND, bool NORM>
-__global__ __launch_bounds__(256) void row_kernel(GemmTable tab, int Bp) {
+__global__ __launch_bounds__(256) void row_kernel(int Bp, GemmTable tab) {   // Bp first: preloaded
   const GemmProb& P = tab.p[blockIdx.y];
   // grid.x = Bp / 4 exactly (launch_rows): every wave owns a row, no bounds check (which would put
   // a kernel-argument round trip ahead of the row's loads)
@@ -1079,23 +1085,34 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void lnbwd_rows_kernel(const LnBwdProb* __restrict__ probs, int Bp,
-                                                         int norm) {
+// templated on NORM and with the problems in the kernel arguments: a runtime `norm` select on
+// the statistics loads compiled to a branch and a load drain per row (5 dependent load rounds)
+template <bool NORM>
+__global__ __launch_bounds__(256) void lnbwd_rows_kernel(int Bp, LnBwdTable tab) {   // Bp first: preloaded
   constexpr int RB = 4;
-  const LnBwdProb P = probs[blockIdx.y];
+  const LnBwdProb& P = tab.p[blockIdx.y];
   const int lane = threadIdx.x & 63;
+  // grid.x = Bp / 16 exactly (Bp is a multiple of 32): no bounds check, which would put a
+  // kernel-argument round trip ahead of the table's
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RB;
-  if (row0 >= Bp) return;
   float gu[RB][8], h[RB][8], g[8], mean[RB], rstd[RB];
-  if (norm) rv_load(g, P.lng, P.ld, lane);
+  float4 qg[2], qu[RB][2], qh[RB][2];
+  if constexpr (NORM) rv_load_raw(qg, P.lng, P.ld, lane);
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
-    rv_load(gu[r], P.GU + (size_t)(row0 + r) * P.ld, P.ld, lane);
-    rv_load(h[r], P.H + (size_t)(row0 + r) * P.ld, P.ld, lane);
-    mean[r] = norm ? gld(P.stats + (row0 + r)) : 0.f;
-    rstd[r] = norm ? gld(P.stats + (Bp + row0 + r)) : 1.f;
+    rv_load_raw(qu[r], P.GU + (size_t)(row0 + r) * P.ld, P.ld, lane);
+    rv_load_raw(qh[r], P.H + (size_t)(row0 + r) * P.ld, P.ld, lane);
+    mean[r] = NORM ? gld(P.stats + (row0 + r)) : 0.f;
+    rstd[r] = NORM ? gld(P.stats + (Bp + row0 + r)) : 1.f;
   }
-  if (norm) ln_bwd_rows_pk<RB>(gu, h, g, mean, rstd, 1.0f / (float)P.K);
+  __builtin_amdgcn_sched_barrier(0);     // every load requested before the first use
+  if constexpr (NORM) rv_from_raw(g, qg, P.ld, lane);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    rv_from_raw(gu[r], qu[r], P.ld, lane);
+    rv_from_raw(h[r], qh[r], P.ld, lane);
+  }
+  if constexpr (NORM) ln_bwd_rows_pk<RB>(gu, h, g, mean, rstd, 1.0f / (float)P.K);
   else ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.K, lane, 0);
 #pragma unroll
   for (int r = 0; r < RB; ++r) rv_store(P.GZ + (size_t)(row0 + r) * P.ld, P.ld, lane, gu[r]);
@@ -1564,18 +1581,18 @@ template <bool NORM>
 static void launch_rows_t(int kind, const GemmTable& d, int Bp, hipStream_t s) {
   const dim3 grid(Bp / 4, d.nprob);
   switch (kind) {
-    case kRowPolicyHead: hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(256), 0, s, d, Bp); break;
-    case kRowCriticLoss: hipLaunchKernelGGL((row_kernel<kRowCriticLoss, NORM>), grid, dim3(256), 0, s, d, Bp); break;
-    case kRowActorLoss: hipLaunchKernelGGL((row_kernel<kRowActorLoss, NORM>), grid, dim3(256), 0, s, d, Bp); break;
+    case kRowPolicyHead: hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(256), 0, s, Bp, d); break;
+    case kRowCriticLoss: hipLaunchKernelGGL((row_kernel<kRowCriticLoss, NORM>), grid, dim3(256), 0, s, Bp, d); break;
+    case kRowActorLoss: hipLaunchKernelGGL((row_kernel<kRowActorLoss, NORM>), grid, dim3(256), 0, s, Bp, d); break;
     case kRowActorHeadBwd:
-      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(256), 0, s, d, Bp);
+      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(256), 0, s, Bp, d);
       break;
     case kRowCriticLossP:
-      hipLaunchKernelGGL((row_kernel<kRowCriticLossP, NORM>), grid, dim3(256), 0, s, d, Bp);
+      hipLaunchKernelGGL((row_kernel<kRowCriticLossP, NORM>), grid, dim3(256), 0, s, Bp, d);
       break;
-    case kRowActorLossP: hipLaunchKernelGGL((row_kernel<kRowActorLossP, NORM>), grid, dim3(256), 0, s, d, Bp); break;
+    case kRowActorLossP: hipLaunchKernelGGL((row_kernel<kRowActorLossP, NORM>), grid, dim3(256), 0, s, Bp, d); break;
     case kRowActorHeadBwdP:
-      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwdP, NORM>), grid, dim3(256), 0, s, d, Bp);
+      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwdP, NORM>), grid, dim3(256), 0, s, Bp, d);
       break;
     default: break;
   }
@@ -1600,8 +1617,13 @@ int launch_heads(const HeadArgs& a, int nprob, hipStream_t s) {
   return 0;
 }
 
-int launch_lnbwd_rows(const LnBwdProb* d, int nprob, int Bp, int norm, hipStream_t s) {
-  hipLaunchKernelGGL(lnbwd_rows_kernel, dim3((Bp + 15) / 16, nprob), dim3(256), 0, s, d, Bp, norm);
+int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s) {
+  if (nprob < 1 || nprob > kMaxLnBwd || Bp % 16 != 0) {
+    set_error("launch_lnbwd_rows: %d problems (max %d), Bp %d (multiple of 16)", nprob, kMaxLnBwd, Bp);
+    return -1;
+  }
+  if (norm) hipLaunchKernelGGL(lnbwd_rows_kernel<true>, dim3(Bp / 16, nprob), dim3(256), 0, s, Bp, tab);
+  else hipLaunchKernelGGL(lnbwd_rows_kernel<false>, dim3(Bp / 16, nprob), dim3(256), 0, s, Bp, tab);
   TD3_HIP(hipGetLastError());
   return 0;
 }

@@ -553,7 +553,8 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
                            flops, std::string(tag) + "_bwd" + std::to_string(l), nullptr, 0));
   }
   if (need_dz0 && !need_in) {
-    std::vector<LnBwdProb> probs;
+    LnBwdTable tab{};
+    int np = 0;
     for (auto& it : items) {
       const LinearL& L = it.net->lin[0];
       LnBwdProb p{};
@@ -564,15 +565,15 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.ld = L.Np;
       p.K = L.N;
       p.GZ = it.e->GZ[0];
-      probs.push_back(p);
+      if (np == kMaxLnBwd) {
+        set_error("%s_lnbwd0: more than %d networks", tag, kMaxLnBwd);
+        return -1;
+      }
+      tab.p[np++] = p;
     }
-    void* d = nullptr;
-    TD3_RC(upload(h, owned, probs.data(), probs.size() * sizeof(LnBwdProb), &d));
-    const int np = (int)probs.size();
-    const LnBwdProb* dp = (const LnBwdProb*)d;
     const int nrm = norm ? 1 : 0;
     st.push_back({std::string(tag) + "_lnbwd0",
-                  [=](hipStream_t s) { return launch_lnbwd_rows(dp, np, Bp, nrm, s); }, 0,
+                  [=](hipStream_t s) { return launch_lnbwd_rows(tab, np, Bp, nrm, s); }, 0,
                   "td3::lnbwd_rows_kernel"});
   }
   return 0;
