@@ -348,10 +348,23 @@ constexpr int kHeadRegs = 8;   // head outputs kept in registers (wider heads lo
 
 template <bool NORM>
 __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx& c) {
+  // every field in one scalar-load batch, and the step counter (Philox noise) requested with
+  // the row: left alone, the compiler fetched fields where used (a chain of kernel-argument round
+  // trips) and the counter after the head's dot products (one more memory round trip at the tail)
+  asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]),
+               "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.exi[0]),
+               "s"(P.exi[1]), "s"(P.exi[2]), "s"(P.exi[3]), "s"(P.exi[4]), "s"(P.exi[5]), "s"(P.exi[6]),
+               "s"(P.exi[7]), "s"(P.exi[8]), "s"(P.exi[9]), "s"(P.exf[0]), "s"(P.exf[1]), "s"(P.exf[2]),
+               "s"(P.seed), "s"(P.ctr), "s"(P.B));
   const int K3 = P.exi[0], ld3 = P.exi[1], ldw4 = P.exi[2];
   const int ad = P.exi[5], sd = P.exi[6];
   const bool target = P.exi[8] != 0;
   const float ma = P.exf[0];
+  const bool gen = target && P.exi[4];
+  // the counter by an asm load into VGPRs (ctr is always set, td3.hip): a plain load of this
+  // uniform value is copied to SGPRs at once, i.e. waited for ahead of the row's loads
+  uint64_t stepv;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(stepv) : "v"(&P.ctr->total_it) : "memory");
   float x[1][8], g[8], bb[8], mean[1], rstd[1];
   float w4[kHeadRegs][8], b4v[kHeadRegs];
   rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
@@ -398,9 +411,10 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   float a;
   if (target) {
     float z = nz;
-    if (P.exi[4]) {                                          // Philox N(0,1) (randn_like, :132)
+    if (gen) {                                               // Philox N(0,1) (randn_like, :132)
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(stepv) :: "memory");
       float g4[4];
-      philox_normal4(P.seed, (uint64_t)P.ctr->total_it, kStreamNoise, (uint32_t)(c.row * 8 + (o >> 2)), g4);
+      philox_normal4(P.seed, stepv, kStreamNoise, (uint32_t)(c.row * 8 + (o >> 2)), g4);
       z = g4[o & 3];
       gst(P.ex[5] + ((size_t)c.row * P.exi[7] + o), z);
     }
@@ -424,6 +438,13 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
 // exi[0]=K3 exi[1]=ld3 exi[2]=j   exf[0]=discount exf[1]=2/B
 template <bool NORM>
 __device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx& c) {
+  // every field in one scalar-load batch (left alone: a kernel-argument round trip per pointer)
+  asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]),
+               "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.ex[11]),
+               "s"(P.ex[12]), "s"(P.ex[13]), "s"(P.ex[14]), "s"(P.ex[15]), "s"(P.ex[16]));
+  asm volatile("" ::"s"(P.ex[17]), "s"(P.ex[18]), "s"(P.ex[19]), "s"(P.ex[20]), "s"(P.ex[21]), "s"(P.ex[22]),
+               "s"(P.ex[23]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[2]), "s"(P.exf[0]), "s"(P.exf[1]),
+               "s"(P.Aout), "s"(P.ldao), "s"(P.B));
   const int K3 = P.exi[0], ld3 = P.exi[1], j = P.exi[2];
   float x0[1][8], x1[1][8], xq[1][8], h[1][8], g[3][8], bb[3][8], w[3][8];
   rv_load(x0[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
@@ -439,6 +460,7 @@ __device__ __forceinline__ void row_critic_loss(const GemmProb& P, const RowCtx&
   }
   const float b40 = gld(P.ex[12]), b41 = gld(P.ex[13]), b4q = gld(P.ex[14]);
   const float rw = gld(P.ex[15] + c.row), nd = gld(P.ex[16] + c.row);
+  __builtin_amdgcn_sched_barrier(0);     // every load requested before the first use
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) h[0][jj] = xq[0][jj];
   float m0[1], s0[1], m1[1], s1[1], mq[1], sq[1];
@@ -773,6 +795,7 @@ __global__ __launch_bounds__(256) void row_kernel(int Bp, GemmTable tab) {   // 
   // grid.x = Bp / 4 exactly (launch_rows): every wave owns a row, no bounds check (which would put
   // a kernel-argument round trip ahead of the row's loads)
   const RowCtx c{(int)(blockIdx.x * 4 + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
+  TL_MARK(0);
   if constexpr (KIND == kRowPolicyHead) row_policy_head<NORM>(P, c);
   else if constexpr (KIND == kRowCriticLoss) row_critic_loss<NORM>(P, c);
   else if constexpr (KIND == kRowActorLoss) row_actor_loss<NORM>(P, c);
@@ -780,6 +803,7 @@ __global__ __launch_bounds__(256) void row_kernel(int Bp, GemmTable tab) {   // 
   else if constexpr (KIND == kRowCriticLossP) row_critic_loss_p<NORM>(P, c);
   else if constexpr (KIND == kRowActorLossP) row_actor_loss_p<NORM>(P, c);
   else if constexpr (KIND == kRowActorHeadBwdP) row_actor_head_bwd_p<NORM>(P, c);
+  TL_MARK(3);
 }
 
 // ================================================================== batch-row GEMM stage

@@ -57,6 +57,17 @@ def main():
             t = C.c_float()
             _lib.check(lib.td3_time_stage(h, i, 20, C.byref(t)), "time")
             ev = t.value * 1e3
+            if "row_kernel" in kern:
+                lib.td3_tl_clear()
+                _lib.check(lib.td3_time_stage(h, i, 1, C.byref(t)), "time1")
+                lib.td3_tl_read(buf.ctypes.data, 8192)
+                v = buf[(buf[:, 3] != 0)].astype(np.int64)
+                base = v[:, 0].min()
+                dur = (v[:, 3] - v[:, 0]) * 0.01
+                print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f} {len(v):4d} {(v[:, 3].max() - base) * 0.01:6.2f} "
+                      f"{(v[:, 0].max() - base) * 0.01:6.2f}   wave-0 dur p10/50/90 "
+                      f"{np.round(np.percentile(dur, [10, 50, 90]), 2).tolist()}")
+                continue
             if "gemm_kernel" not in kern and kern != "td3::dw_kernel":
                 print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f}")
                 continue
