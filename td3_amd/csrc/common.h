@@ -79,10 +79,14 @@ __device__ __forceinline__ void philox_normal4(uint64_t seed, uint64_t step, uin
   u32x4 c{idx, stream, (uint32_t)step, (uint32_t)(step >> 32)};
   u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   float u1 = u01_open(r.x), u2 = u01_open(r.y), u3 = u01_open(r.z), u4 = u01_open(r.w);
-  float rad1 = sqrtf(-2.0f * logf(u1)), rad2 = sqrtf(-2.0f * logf(u3));
-  float s1, c1, s2, c2;
-  sincospif(2.0f * u2, &s1, &c1);
-  sincospif(2.0f * u4, &s2, &c2);
+  // hardware transcendentals (v_log_f32 = log2, v_sqrt_f32, v_sin / v_cos_f32 of revolutions):
+  // u is in [2^-24, 1], so the libm range / denormal fix-ups (a long chain on the policy head's
+  // tail) are not needed
+  constexpr float kM2Ln2 = -2.0f * 0.693147180559945f;
+  const float rad1 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u1));
+  const float rad2 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u3));
+  const float s1 = __builtin_amdgcn_sinf(u2), c1 = __builtin_amdgcn_cosf(u2);
+  const float s2 = __builtin_amdgcn_sinf(u4), c2 = __builtin_amdgcn_cosf(u4);
   out[0] = rad1 * c1;
   out[1] = rad1 * s1;
   out[2] = rad2 * c2;

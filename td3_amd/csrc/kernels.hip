@@ -380,6 +380,8 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   }
   float nz = 0.f;
   if (target && !P.exi[4] && c.lane < ad) nz = gld(P.ex[5] + ((size_t)c.row * P.exi[7] + c.lane));
+  TL_MARK(5);
+  TL_FINE(6);
   if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
   float mine = 0.f;                       // lane o keeps head output o
   float part[kHeadRegs];
@@ -404,6 +406,7 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
       gst(P.ex[9] + (c.Bp + c.row), rstd[0]);
     }
   }
+  TL_MARK(7);
   if (c.lane >= ad) return;
   const int o = c.lane;
   const bool live = c.row < P.B;

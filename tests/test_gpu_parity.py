@@ -231,6 +231,22 @@ def test_philox_graph_path_teacher_forced(name):
     assert len(seen) == 4                                   # a fresh draw every step
 
 
+def test_philox_noise_is_standard_normal():
+    """The target-smoothing noise the step draws (Philox + Box-Muller on the hardware
+    transcendentals): N(0, 1) by a Kolmogorov-Smirnov test over 8 steps, a fresh draw per step."""
+    from scipy import stats as st
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    draws = []
+    for _ in range(8):
+        out = pol.train_step(rb, S["B"], stats=True)
+        draws.append(out["noise"].ravel())
+    z = np.concatenate(draws).astype(np.float64)
+    assert len({d.tobytes() for d in draws}) == len(draws)
+    assert abs(z.mean()) < 5.0 / np.sqrt(z.size) and abs(z.std() - 1.0) < 0.05
+    assert st.kstest(z, "norm").pvalue > 1e-4
+
+
 def test_allreduce_path_single_rank():
     """The data-parallel kernels (grad-only dW, RCCL all-reduce, flat Adam + Polyak) at
     nranks = 1 against the oracle, teacher-forced like the fused path."""

@@ -67,6 +67,10 @@ def main():
                 print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f} {len(v):4d} {(v[:, 3].max() - base) * 0.01:6.2f} "
                       f"{(v[:, 0].max() - base) * 0.01:6.2f}   wave-0 dur p10/50/90 "
                       f"{np.round(np.percentile(dur, [10, 50, 90]), 2).tolist()}")
+                for k in (5, 6, 7):
+                    if v[:, k].min() > 0:
+                        print(f"   mark{k} {np.median(v[:, k] - v[:, 0]) * 0.01:5.2f}", end="")
+                print()
                 continue
             if "gemm_kernel" not in kern and kern != "td3::dw_kernel":
                 print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f}")
