@@ -268,15 +268,21 @@ __device__ __forceinline__ void l0_put_x(const GemmProb& P, const RingSide& rs, 
   }
 }
 
+// k offset of lane half h in the layer-0 operands: 12h when the input fits in 24 columns (the x
+// rows' and W0 rows' columns 24..31 are zero pads, so a half's 16-wide read past k = 24 reads 0)
+__device__ __forceinline__ int l0_koff(const GemmProb& P, int h) { return (P.exi[6] <= 24 ? 12 : 16) * h; }
+
 // Stage 2: Z0 = X * W0^T on MFMA (wave w: layer-0 column tiles w and w + 8), + b0, ReLU, into the
 // layer-1 A buffer (LDS, [32][S]); n-tile 0 also stores H0 (the backward's post-ReLU rows).
-// (Halving the MFMAs by laying the K0 <= 24 inputs out as k = 12h + s cost more in operand
-// shuffles than the 4 MFMAs per tile it saved: TF_fwd01 12.3 -> 12.4-14 us.)
+// K0 <= 24 (every featured input but the widest): lane half h supplies k = 12h + s, so 12 MFMAs
+// cover the row instead of 16 -- only the operand offsets change (l0_koff), no shuffles.  (An
+// earlier variant that selected between layouts on the loaded data waited early: slower.)
 __device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, float* smem, const Ctx& c,
                                         const float (&w0)[2][16], const float (&b0)[2]) {
   const int i = c.lane & 31, h = c.lane >> 5;
   const int n0t = P.exi[5] >> 5;
-  const float* arow = xs + i * kL0XS + 16 * h;
+  const bool k24 = P.exi[6] <= 24;
+  const float* arow = xs + i * kL0XS + l0_koff(P, h);
   float av[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -293,7 +299,11 @@ __device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, floa
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], w0[ct][s], acc);
+    for (int s = 0; s < 12; ++s) acc = mfma32x32x2(av[s], w0[ct][s], acc);
+    if (!k24) {
+#pragma unroll
+      for (int s = 12; s < 16; ++s) acc = mfma32x32x2(av[s], w0[ct][s], acc);
+    }
     const int col = tile * 32 + i;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -924,10 +934,11 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   if constexpr (kL0) l0_load_x<PRO == kProL0G>(P, tab.rs, c, l0x);
   float w0[2][16], b0v[2];
   if constexpr (kL0) {
+    const int koff = l0_koff(P, h);
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       const int tile = min(wave + kNW * ct, (P.exi[5] >> 5) - 1);
-      const float* wp = P.ex[8] + (size_t)(tile * 32 + i) * 32 + 16 * h;
+      const float* wp = P.ex[8] + (size_t)(tile * 32 + i) * 32 + koff;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 v = gld4(wp + 4 * q);

@@ -27,6 +27,12 @@ def load_golden(kind, name):
 
 def featured_setup(name):
     sd, ad, ma, norm, B, steps, hp = gen.FEATURED_CONFIGS[name]
+    return featured_setup_dims(sd, ad, ma, norm, B, steps, hp)
+
+
+def featured_setup_dims(sd, ad, ma=1.0, norm="layer", B=256, steps=2, hp=None):
+    """A featured setup of any state / action width (no golden fixture: oracle-only parity)."""
+    hp = dict(hp or {})
     a0 = gen.init_params(gen.featured_actor_shapes(sd, ad, norm), gen.SEED)
     c0 = gen.init_params(gen.featured_critic_shapes(sd, ad, norm), gen.SEED + 100)
     buf = orc.FeaturedBuffer(sd, ad, gen.BUFFER_ROWS)

@@ -8,7 +8,7 @@ the tensor scale), gradients rtol 1e-4, post-Adam parameters within 1e-6 + 1e-5|
 import numpy as np
 import pytest
 
-from helpers import gen, orc, load_golden, featured_setup
+from helpers import featured_setup_dims, gen, orc, load_golden, featured_setup
 
 pytestmark = pytest.mark.gpu
 
@@ -269,6 +269,27 @@ def test_allreduce_path_single_rank():
         _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (p, "actor"))
         _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"))
         _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"))
+
+
+@pytest.mark.parametrize("sd,ad", [(24, 4), (29, 3)])
+def test_layer0_widths_teacher_forced(sd, ad):
+    """Network inputs of 25..32 columns: the fused layer 0 runs its 16-MFMA K layout (inputs of
+    <= 24 columns, every golden config, use 12 MFMAs per tile, kernels.hip l0_koff)."""
+    S = featured_setup_dims(sd, ad)
+    pol, rb = _make(S)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    rs = np.random.RandomState(sd)
+    for step in (1, 2):
+        idx = rs.randint(0, gen.BUFFER_ROWS, S["B"])
+        noise = rs.standard_normal((S["B"], ad)).astype(np.float32)
+        _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        out = pol.train_step(rb, S["B"], indices=idx, noise=noise, stats=True)
+        assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5, (step, "y")
+        assert _rel_to_max(out["q1"], rec["q1"][:, 0]) <= 1e-5, (step, "q1")
+        np.testing.assert_allclose(out["critic_loss"], rec["critic_loss"], rtol=1e-5)
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (step, "critic"))
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
 
 
 @pytest.mark.parametrize("B", [512, 1024])
