@@ -856,6 +856,32 @@ __device__ __forceinline__ void load_b(const GemmProb& P, float (&bv)[NCH][16], 
   for (int cc = 0; cc < NCH; ++cc) load_chunk<MODE>(P, bv[cc], min(cb + cc, nch - 1), ncol, h);
 }
 
+// WN = 0 (16 columns, v_mfma_f32_16x16x4_f32): lane (column ncol, k-group g) holds the weights
+// k = ch*32 + 8g + s, s = 0..7, in b[0..7] (MODE 0: W[n][k], two float4; MODE 1: W[k][n]).
+template <int MODE>
+__device__ __forceinline__ void load_chunk16(const GemmProb& P, float (&b)[16], int ch, int ncol, int g) {
+  const int kb = ch * 32 + 8 * g;
+  if (MODE == 0) {
+    const float* wp = P.W + (size_t)ncol * P.ldw + kb;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float4 v = gld4(wp + 4 * q);
+      b[4 * q + 0] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+    }
+  } else {
+    const float* wp = P.W + (size_t)kb * P.ldw + ncol;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) b[s] = gld(wp + (size_t)s * P.ldw);
+  }
+}
+
+template <int MODE, int NCH>
+__device__ __forceinline__ void load_b16(const GemmProb& P, float (&bv)[NCH][16], int cb, int nch,
+                                         int ncol, int g) {
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) load_chunk16<MODE>(P, bv[cc], min(cb + cc, nch - 1), ncol, g);
+}
+
 // XCD-aware tile order (cdna_hip_programming.md §5.5 T1): the dispatcher deals blocks
 // round-robin over the 8 XCDs, so block b runs on XCD b % 8.  Consecutive tiles (which share
 // a weight column block: m is the fastest tile index) are given to blocks of one XCD, so a
@@ -877,9 +903,13 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
                                                         GemmTable tab, Counters* bump, int bump_actor) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
-  constexpr int WK = kNW / WN;
+  // WN = 0: 16 output columns per workgroup on v_mfma_f32_16x16x4_f32 (two 16-row halves of the
+  // 32-row tile): half the MFMA chain of WN = 1 for stages of <= 128 32-column workgroups, which
+  // otherwise leave half the CUs idle (td3.hip gemm_wn)
+  constexpr int WNS = WN == 0 ? 1 : WN;        // waves per K group
+  constexpr int WK = kNW / WNS;
   constexpr int NT = 64 * kNW;                 // threads
-  constexpr int OUTW = 32 * WN;                // output columns of the workgroup
+  constexpr int OUTW = WN == 0 ? 16 : 32 * WN; // output columns of the workgroup
   constexpr bool kPrefetchB = true;
   const int b = xcd_tile(nb);
   TL_MARK(0);
@@ -908,17 +938,17 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
   const int m0 = mt << 5;
-  const int n0 = nt * 32 * WN;
+  const int n0 = nt * OUTW;
   const int Kp = P.Kp;
   const int S = lds_stride(Kp);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = lane & 31, h = lane >> 5;
-  const int wn = wave % WN, wk = wave / WN;
+  const int wn = wave % WNS, wk = wave / WNS;
   const int nch = Kp >> 5;
   const int cb = wk * nch / WK, ce = (wk + 1) * nch / WK;
   const int ncol0 = n0 + wn * 32;
   const bool active = ncol0 < P.Nout;
-  const int ncol = (active ? ncol0 : 0) + i;
+  const int ncol = (active ? ncol0 : 0) + (WN == 0 ? (lane & 15) : i);
 
   // weight chunks requested at the kernel start (the rest stream in the MFMA loop).  Prefetching
   // all 4 chunks of a WN=2 wave was no faster: the A-row loads then queue behind 16 weight loads.
@@ -948,7 +978,8 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     }
   }
   if constexpr (kPrefetchB) {
-    load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
+    if constexpr (WN == 0) load_b16<MODE, kCh>(P, bv, cb, nch, ncol, lane >> 4);
+    else load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
   }
 
@@ -991,10 +1022,40 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     if (s0 + 1 < ce) load_chunk<MODE>(P, bs1, s0 + 1, ncol, h);
   }
 
+  f32x4 acc16[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // WN = 0: rows 0-15, 16-31
+  if constexpr (WN == 0) {
+    if (active) {
+      // lane (r = lane & 15, g = lane >> 4) supplies k = kb + 8g + s of MFMA s: its 8 A values
+      // of a row are contiguous (2 ds_read_b128) and its 8 weights too; the two row halves are
+      // independent accumulators (40-cycle dependent latency vs 32-cycle issue)
+      const int g = lane >> 4;
+      const float* ar0 = smem + (lane & 15) * S + 8 * g;
+      const float* ar1 = ar0 + 16 * S;
+#pragma unroll
+      for (int cc = 0; cc < kCh; ++cc) {
+        if (cb + cc < ce) {
+          const int kb = (cb + cc) * 32;
+          float x0[8], x1[8];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const float4 u = *reinterpret_cast<const float4*>(ar0 + kb + 4 * q);
+            const float4 v = *reinterpret_cast<const float4*>(ar1 + kb + 4 * q);
+            x0[4 * q + 0] = u.x; x0[4 * q + 1] = u.y; x0[4 * q + 2] = u.z; x0[4 * q + 3] = u.w;
+            x1[4 * q + 0] = v.x; x1[4 * q + 1] = v.y; x1[4 * q + 2] = v.z; x1[4 * q + 3] = v.w;
+          }
+#pragma unroll
+          for (int s = 0; s < 8; ++s) {
+            acc16[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[s], bv[cc][s], acc16[0], 0, 0, 0);
+            acc16[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[s], bv[cc][s], acc16[1], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  if (active) {
+  if (WN != 0 && active) {
     const float* arow = smem + i * S + 16 * h;
 #pragma unroll
     for (int cc = 0; cc < kCh; ++cc) {
@@ -1036,7 +1097,7 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     }
   }
 
-  if constexpr (WK == 1) {
+  if constexpr (WK == 1 && WN != 0) {
     if (active) {
       const int col = ncol0 + i;
 #pragma unroll
@@ -1051,9 +1112,18 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     TL_MARK(2);
   } else {
     __syncthreads();
-    float* red = smem;  // [kNW][32][33]; wave = wk * WN + wn
+    float* red = smem;  // [kNW][32][33]; wave = wk * WNS + wn
+    if constexpr (WN == 0) {
+      // 16x16 C/D map: column lane & 15, row 4 * (lane >> 4) + j
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          red[(wave * 32 + 16 * half + 4 * (lane >> 4) + j) * 33 + (lane & 15)] = acc16[half][j];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
+    }
     __syncthreads();
     TL_MARK(2);
 #pragma unroll
@@ -1063,7 +1133,7 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
       const int wnn = colw >> 5, ci = colw & 31;
       float v = red[(wnn * 32 + row) * 33 + ci];
 #pragma unroll
-      for (int w = 1; w < WK; ++w) v = v + red[((w * WN + wnn) * 32 + row) * 33 + ci];
+      for (int w = 1; w < WK; ++w) v = v + red[((w * WNS + wnn) * 32 + row) * 33 + ci];
       if (MODE == 0 && P.bias) v = v + bias;
       if (P.relu) v = fmaxf(v, 0.f);
       if (n0 + colw < P.Nout) gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + colw), v);
@@ -1593,6 +1663,8 @@ static GemmFn pick_bwd(int pro) {
 }
 
 static GemmFn pick_gemm(int mode, int wn, int pro) {
+  if (mode == 0 && wn == 0) return pick_fwd<0>(pro);
+  if (mode == 1 && wn == 0) return pick_bwd<0>(pro);
   if (mode == 0 && wn == 1) return pick_fwd<1>(pro);
   if (mode == 0 && wn == 2) return pick_fwd<2>(pro);
   if (mode == 0 && wn == 4) return pick_fwd<4>(pro);
@@ -1709,7 +1781,8 @@ static int set_attr_all() {
 }
 
 int kernels_init() {
-  int rc = set_attr_all<1>();
+  int rc = set_attr_all<0>();
+  if (!rc) rc = set_attr_all<1>();
   if (!rc) rc = set_attr_all<2>();
   if (!rc) rc = set_attr_all<4>();
   return rc;

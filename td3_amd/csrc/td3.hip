@@ -359,14 +359,21 @@ static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<
 //   * B = 256 forward stages (3-4 networks): 64 columns (WN=2): HalfCheetah F_fwd1 15.0 ->
 //     13.8 us, F_fwd2 13.9 -> 12.4 us; WN=4 there is slower (18.3 us), and the input-grad
 //     stages (strided weight reads) lose with WN=2 (CB_bwd1 9.0 -> 10.8 us).
-// Narrow K (<= 128) always uses WN=4.
+// Narrow K (<= 128) always uses WN=4.  A stage of <= 128 32-column workgroups (one- and
+// two-network B=256 layers) leaves half the CUs idle: 16 columns per workgroup (WN=0,
+// v_mfma_f32_16x16x4_f32) doubles the workgroups and halves each one's MFMA chain.
 #ifndef TD3_WN2_MIN
 #define TD3_WN2_MIN 256
 #endif
+#ifndef TD3_WN0_MAX
+#define TD3_WN0_MAX 128
+#endif
 static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd) {
   if (maxK <= 128 || (Bp >= 512 && wn1_blocks >= 256)) return 4;
+  if (wn1_blocks <= TD3_WN0_MAX) return 0;
   return (fwd && wn1_blocks >= TD3_WN2_MIN) ? 2 : 1;
 }
+static int gemm_outw(int wn) { return wn == 0 ? 16 : 32 * wn; }   // output columns per workgroup
 
 // Forward layers 0..2 of several networks (one launch per layer); layer 0 copies the
 // network input rows, layers 1 and 2 apply the previous layer's LayerNorm in the prologue.
@@ -477,7 +484,7 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.C = it.e->H[l];
       p.ldc = L.Np;
       p.relu = 1;
-      p.ntiles = (L.Np + 32 * wn - 1) / (32 * wn);
+      p.ntiles = (L.Np + gemm_outw(wn) - 1) / gemm_outw(wn);
       p.tile_begin = blocks;
       blocks += (Bp / 32) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
@@ -542,7 +549,7 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.C = l > 0 ? it.e->GU[l - 1] : it.e->GUin;
       p.ldc = L.Kp;
       p.relu = 0;
-      p.ntiles = (L.Kp + 32 * wn - 1) / (32 * wn);
+      p.ntiles = (L.Kp + gemm_outw(wn) - 1) / gemm_outw(wn);
       p.tile_begin = blocks;
       blocks += (Bp / 32) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
