@@ -158,6 +158,17 @@ __device__ __forceinline__ void rv_load_u(float (&v)[8], const float* __restrict
 // A problem's first column tile also stores its rows for the later stages (no extra loads):
 // Aout (+ ex[0], ld exi[3]) = the A row; ex[1] / ex[2] = reward / not_done (record offset
 // exi[1], exi[1] + 1); problem 0 records the drawn rows.
+
+// reward (lane 0) / not_done (lane 1) destination of the sample: a select between the two
+// scalar fields.  Indexed as P.ex[1 + lane], the pointer was fetched by a VECTOR load of the
+// kernel arguments whose vmcnt(0) drained every weight load in flight (the n-tile-0 workgroups
+// of F_fwd01 ran ~3 us behind the rest).
+__device__ __forceinline__ float* rw_ptr(const GemmProb& P, int lane) {
+  float* r0 = P.ex[1];
+  float* r1 = P.ex[2];
+  asm volatile("" : "+s"(r0), "+s"(r1));   // pinned in SGPRs: the select below is a v_cndmask
+  return lane == 0 ? r0 : r1;
+}
 __device__ __forceinline__ void pro_gather(const GemmProb& P, const RingSide& rs, float* smem, const Ctx& c,
                                            int pi) {
   const uint64_t step = (uint64_t)(rs.ctr->total_it + 1);
@@ -176,7 +187,7 @@ __device__ __forceinline__ void pro_gather(const GemmProb& P, const RingSide& rs
     if (idx[r] >= 0) {
       const float* rec = rs.data + (size_t)idx[r] * rs.rec;
       rv_load_u(x[r], rec + P.exi[0], P.Kreal, c.lane);
-      if (t0 && c.lane < 2 && P.ex[1 + c.lane]) rw[r] = gld(rec + P.exi[1] + c.lane);
+      if (t0 && c.lane < 2 && rw_ptr(P, c.lane)) rw[r] = gld(rec + P.exi[1] + c.lane);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[r][j] = 0.f;
@@ -196,7 +207,7 @@ __device__ __forceinline__ void pro_gather(const GemmProb& P, const RingSide& rs
         if (P.ex[0]) gst(P.ex[0] + (size_t)grow * P.exi[3] + col, x[r][j]);
       }
     }
-    if (c.lane < 2 && P.ex[1 + c.lane]) gst(P.ex[1 + c.lane] + grow, rw[r]);
+    if (c.lane < 2 && rw_ptr(P, c.lane)) gst(rw_ptr(P, c.lane) + grow, rw[r]);
     if (pi == 0 && rs.idx_out && c.lane == 0 && grow < P.B) rs.idx_out[grow] = idx[r];
   }
 }
@@ -224,23 +235,33 @@ __device__ __forceinline__ void l0_load_x(const GemmProb& P, const RingSide& rs,
   }
   const int col = i;
   const bool valid = i < K0;
+  // every row's index is drawn before the first record load: drawn row by row, the second draw
+  // (which reads the loaded step / ring size) sat behind a vmcnt(0) that also drained the first
+  // row's record load
+  if constexpr (GATHER) {
+#pragma unroll
+    for (int rr = 0; rr < kL0R; ++rr) {
+      const int grow = c.m0 + c.wave * kRPW + 2 * rr + h;
+      X.idx[rr] = grow < P.B ? (int64_t)philox_index(rs.seed, step, (uint32_t)grow, n) : -1;
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // unconditional loads (padding rows read ring row 0, padding columns a real column) masked in
+  // l0_put_x: conditional loads put the waitcnt pass's vmcnt(0) at their control-flow joins,
+  // draining the record loads before the weights were even requested
 #pragma unroll
   for (int rr = 0; rr < kL0R; ++rr) {
     const int row = c.wave * kRPW + 2 * rr + h, grow = c.m0 + row;
-    X.x[rr] = 0.f;
-    X.rw[rr] = 0.f;
     if constexpr (GATHER) {
-      const int64_t idx = grow < P.B ? (int64_t)philox_index(rs.seed, step, (uint32_t)grow, n) : -1;
-      X.idx[rr] = idx;
-      if (idx >= 0) {
-        const float* rec = rs.data + (size_t)idx * rs.rec;
-        if (valid) X.x[rr] = gld(rec + P.exi[0] + col);
-        if (t0 && i < 2 && P.ex[1 + i]) X.rw[rr] = gld(rec + P.exi[1] + i);
-      }
+      const int64_t idx = X.idx[rr] >= 0 ? X.idx[rr] : 0;
+      const float* rec = rs.data + (size_t)idx * rs.rec;
+      X.x[rr] = gld(rec + P.exi[0] + (valid ? col : 0));
+      X.rw[rr] = t0 ? gld(rec + P.exi[1] + (i & 1)) : 0.f;
     } else {
       X.x[rr] = gld(P.A + (size_t)grow * P.lda + col);  // input rows are >= 32 wide (zero pads)
     }
   }
+  (void)valid;
 }
 
 template <bool GATHER>
@@ -254,14 +275,15 @@ __device__ __forceinline__ void l0_put_x(const GemmProb& P, const RingSide& rs, 
 #pragma unroll
   for (int rr = 0; rr < kL0R; ++rr) {
     const int row = c.wave * kRPW + 2 * rr + h, grow = c.m0 + row;
-    xs[row * kL0XS + i] = X.x[rr];
+    const float xv = (!GATHER || (X.idx[rr] >= 0 && valid)) ? X.x[rr] : 0.f;
+    xs[row * kL0XS + i] = xv;
     if constexpr (GATHER) {
       if (t0) {
         if (valid) {
-          if (P.ex[3]) gst(P.ex[3] + (size_t)grow * P.exi[8] + col, X.x[rr]);
-          if (P.ex[0]) gst(P.ex[0] + (size_t)grow * P.exi[3] + col, X.x[rr]);
+          if (P.ex[3]) gst(P.ex[3] + (size_t)grow * P.exi[8] + col, xv);
+          if (P.ex[0]) gst(P.ex[0] + (size_t)grow * P.exi[3] + col, xv);
         }
-        if (i < 2 && P.ex[1 + i]) gst(P.ex[1 + i] + grow, X.rw[rr]);
+        if (i < 2 && rw_ptr(P, i)) gst(rw_ptr(P, i) + grow, X.idx[rr] >= 0 ? X.rw[rr] : 0.f);
         if (pi == 0 && rs.idx_out && i == 0 && grow < P.B) rs.idx_out[grow] = X.idx[rr];
       }
     }
@@ -277,7 +299,7 @@ __device__ __forceinline__ int l0_koff(const GemmProb& P, int h) { return (P.exi
 // K0 <= 24 (every featured input but the widest): lane half h supplies k = 12h + s, so 12 MFMAs
 // cover the row instead of 16 -- only the operand offsets change (l0_koff), no shuffles.  (An
 // earlier variant that selected between layouts on the loaded data waited early: slower.)
-__device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, float* smem, const Ctx& c,
+__device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, float* smem, float* h0s, const Ctx& c,
                                         const float (&w0)[2][16], const float (&b0)[2]) {
   const int i = c.lane & 31, h = c.lane >> 5;
   const int n0t = P.exi[5] >> 5;
@@ -289,8 +311,7 @@ __device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, floa
     const float4 v = *reinterpret_cast<const float4*>(arow + 4 * q);
     av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
   }
-  float* H0 = P.ex[10];
-  const bool t0 = c.nt == 0;
+  const bool keep = P.ex[10] && P.norm;   // H0 kept in LDS for l0_store_rows (LN overwrites smem)
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     const int tile = c.wave + kNW * ct;
@@ -310,13 +331,13 @@ __device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, floa
       const int row = mfma_row(r, c.lane);
       const float v = fmaxf(acc[r] + b0[ct], 0.f);
       smem[row * c.S + col] = v;
-      if (t0 && H0) gst(H0 + (size_t)(c.m0 + row) * P.exi[5] + col, v);
+      if (keep) h0s[row * c.S + col] = v;
     }
   }
 }
 
 // Stage 3: LayerNorm 0 of the A buffer rows in place (each wave its kRPW rows); n-tile 0 stores
-// U0 (Aout) and the row statistics, as pro_ln.
+// the row statistics, as pro_ln (U0 is stored by l0_store_rows).
 __device__ __forceinline__ void l0_ln(const GemmProb& P, float* smem, const Ctx& c) {
   constexpr int RB = kRPW;
   float x[RB][8], g[8], bb[8], mean[RB], rstd[RB], rm[8];
@@ -331,11 +352,31 @@ __device__ __forceinline__ void l0_ln(const GemmProb& P, float* smem, const Ctx&
   for (int r = 0; r < RB; ++r) {
     const int row = c.wave * kRPW + r, grow = c.m0 + row;
     lds_put_row(smem, c.S, row, P.Kp, c.lane, x[r]);
-    if (t0 && P.Aout) rv_store(P.Aout + (size_t)grow * P.ldao, P.Kp, c.lane, x[r]);
     if (t0 && P.stats && c.lane == 0) {
       gst(P.stats + (grow), mean[r]);
       gst(P.stats + (c.Bp + grow), rstd[r]);
     }
+  }
+}
+
+// Stage 4 (after the layer-1 MFMA loop): H0 (post-ReLU, for LN0's backward) and U0 (post-LN, the
+// layer-1 dW input) of the 32 rows, each n-tile workgroup of the row tile storing its 1/ntiles
+// slice of the columns.  Stored from n-tile 0 during the prologue they were 128 KB of stores
+// queued ahead of its weight stream (vmcnt retires in order): those workgroups ended ~3 us after
+// the rest (F_fwd01, tools/tl_probe.py).
+template <int NT>
+__device__ __forceinline__ void l0_store_rows(const GemmProb& P, const float* smem, const float* h0s, const Ctx& c) {
+  float* H0 = P.ex[10];
+  float* U0 = P.norm ? P.Aout : nullptr;
+  if (!H0 && !U0) return;
+  const float* hsrc = P.norm ? h0s : smem;          // no LN: the A buffer is H0
+  const int nq = P.Kp >> 2;
+  const int q0 = c.nt * nq / P.ntiles, per = (c.nt + 1) * nq / P.ntiles - q0;
+  for (int e = threadIdx.x; e < 32 * per; e += NT) {
+    const int row = e / per, q = 4 * (q0 + e % per);
+    const size_t grow = (size_t)(c.m0 + row);
+    if (H0) gst4(H0 + grow * P.exi[5] + q, *reinterpret_cast<const float4*>(hsrc + row * c.S + q));
+    if (U0) gst4(U0 + grow * P.ldao + q, *reinterpret_cast<const float4*>(smem + row * c.S + q));
   }
 }
 
@@ -937,6 +978,9 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   const int mtiles = Bp >> 5;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
+#if defined(TD3_TL) && !defined(TD3_TL_FINE)
+  if (threadIdx.x == 0 && blockIdx.x < 8192) td3_tl[blockIdx.x][4] |= (unsigned long long)(nt + 1) << 16;
+#endif
   const int m0 = mt << 5;
   const int n0 = nt * OUTW;
   const int Kp = P.Kp;
@@ -1006,7 +1050,7 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     l0_put_x<PRO == kProL0G>(P, tab.rs, xs, c, pi, l0x);
     __syncthreads();
     TL_MARK(6);
-    l0_mfma(P, xs, smem, c, w0, b0v);
+    l0_mfma(P, xs, smem, xs + 32 * kL0XS, c, w0, b0v);
     if (P.norm) {
       __syncthreads();
       TL_MARK(7);
@@ -1097,6 +1141,7 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     }
   }
 
+  if constexpr (kL0) l0_store_rows<NT>(P, smem, smem + 32 * S + 32 * kL0XS, c);
   if constexpr (WK == 1 && WN != 0) {
     if (active) {
       const int col = ncol0 + i;

@@ -488,7 +488,8 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.tile_begin = blocks;
       blocks += (Bp / 32) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
-      lds = std::max(lds, gemm_lds_bytes(L.Kp) + (l0 ? 32 * kL0XS * 4 : 0));
+      // fused layer 0: + the staged input rows and the H0 rows kept for the sliced store
+      lds = std::max(lds, gemm_lds_bytes(L.Kp) + (l0 ? 32 * kL0XS * 4 + 32 * lds_stride(L.Kp) * 4 : 0));
       if (l0) flops += 2.0 * Bp * it.net->lin[0].N * it.net->lin[0].K;
       probs.push_back(p);
     }

@@ -94,7 +94,7 @@ def main():
                 fine += f" mark6 {np.median(t6 - t0) * 0.01:5.2f} mark7 {np.median(t7 - t0) * 0.01:5.2f}"
             print(fine)
             if name in ("F_fwd1", "F_fwd01", "TF_fwd1", "TF_fwd01", "C_dw") and phase == 1:
-                xcc = v[:, 4] & 0xFFFFFFFF
+                xcc = v[:, 4] & 0xFFFF
                 hw = v[:, 4] >> 32
                 print("   per-XCC wg counts:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
                 # HW_ID: wave id [3:0], simd [5:4], pipe [7:6], cu [11:8], sh [12], se [15:13]
@@ -105,6 +105,16 @@ def main():
                 q = np.percentile((t1 - t0) * 0.01, [10, 50, 90])
                 print("   end p10/50/90/max:", np.round(np.percentile((t3 - base) * 0.01, [10, 50, 90, 100]), 2).tolist(),
                       " dur p10/50/90/max:", np.round(np.percentile((t3 - t0) * 0.01, [10, 50, 90, 100]), 2).tolist())
+                ntile = ((v[:, 4] >> 16) & 0xFFFF) - 1
+                if (ntile >= 0).all():
+                    d = (t3 - t0) * 0.01
+                    for nm, sel in (("n-tile 0", ntile == 0), ("others", ntile > 0)):
+                        vv = v[sel]
+                        ph = [np.median(vv[:, k] - vv[:, 0]) * 0.01 for k in (5, 6, 7, 1, 2, 3)]
+                        print(f"   {nm:9s} marks 5,6,7,1,2,3: " + " ".join(f"{x:5.2f}" for x in ph))
+                    print(f"   dur median: n-tile 0 {np.median(d[ntile == 0]):.2f} ({(ntile == 0).sum()} wg), "
+                          f"others {np.median(d[ntile > 0]):.2f}; end median n-tile 0 "
+                          f"{np.median((t3 - base)[ntile == 0]) * 0.01:.2f} others {np.median((t3 - base)[ntile > 0]) * 0.01:.2f}")
                 print("   prologue p10/50/90:", np.round(q, 2).tolist(),
                       " entry p10/50/90:", np.round(np.percentile((t0 - base) * 0.01, [10, 50, 90]), 2).tolist())
 
