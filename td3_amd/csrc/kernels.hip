@@ -338,11 +338,12 @@ __device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, floa
 
 // Stage 3: LayerNorm 0 of the A buffer rows in place (each wave its kRPW rows); n-tile 0 stores
 // the row statistics, as pro_ln (U0 is stored by l0_store_rows).
-__device__ __forceinline__ void l0_ln(const GemmProb& P, float* smem, const Ctx& c) {
+// (gamma / beta are requested at the kernel start: loaded here, their vmcnt wait also drained
+// the n-tile-0 workgroup's sample-copy stores queued ahead of them, ~1 us)
+__device__ __forceinline__ void l0_ln(const GemmProb& P, float* smem, const Ctx& c, const float (&g)[8],
+                                      const float (&bb)[8]) {
   constexpr int RB = kRPW;
-  float x[RB][8], g[8], bb[8], mean[RB], rstd[RB], rm[8];
-  rv_load(g, P.lng, P.Kp, c.lane);
-  rv_load(bb, P.lnb, P.Kp, c.lane);
+  float x[RB][8], mean[RB], rstd[RB], rm[8];
 #pragma unroll
   for (int r = 0; r < RB; ++r) rv_load_lds(x[r], smem + (c.wave * kRPW + r) * c.S, P.Kp, c.lane);
   real_mask(rm, P.Kreal, c.lane);
@@ -1021,6 +1022,13 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
       b0v[ct] = gld(P.ex[9] + tile * 32 + i);
     }
   }
+  float lg[8], lb[8];                          // kL0: LayerNorm-0 gamma / beta
+  if constexpr (kL0) {
+    if (P.norm) {
+      rv_load(lg, P.lng, P.Kp, lane);
+      rv_load(lb, P.lnb, P.Kp, lane);
+    }
+  }
   if constexpr (kPrefetchB) {
     if constexpr (WN == 0) load_b16<MODE, kCh>(P, bv, cb, nch, ncol, lane >> 4);
     else load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
@@ -1054,7 +1062,7 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     if (P.norm) {
       __syncthreads();
       TL_MARK(7);
-      l0_ln(P, smem, c);
+      l0_ln(P, smem, c, lg, lb);
     }
     issue_stream();
   }
