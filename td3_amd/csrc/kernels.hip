@@ -965,17 +965,29 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   // every field this workgroup reads, requested in ONE scalar-load batch: left to itself the
   // compiler requests each where first used, a chain of dependent kernarg round trips ahead of
   // the first operand load (tools/tl_probe.py)
-  asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.H), "s"(P.stats), "s"(P.Aout), "s"(P.W), "s"(P.bias),
-               "s"(P.C), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.ldh), "s"(P.ldao), "s"(P.ldw), "s"(P.Nout),
-               "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.hot_pad));
   constexpr bool kL0 = PRO == kProL0 || PRO == kProL0G;
-  if constexpr (PRO == kProGather || PRO == kProL0G)
-    asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]),
-                 "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
-                 "s"(tab.rs.ctr));
-  if constexpr (kL0)
-    asm volatile("" ::"s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.ex[3]),
-                 "s"(P.exi[8]));
+  if constexpr (kL0) {
+    // fused layer 0: the fields the first operand requests need, in ONE batch (each asm
+    // statement is a use, i.e. a wait: two statements were two dependent round trips); the rest
+    // are batched behind the operand requests (l0_late_fields)
+    if constexpr (PRO == kProL0G)
+      asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
+                   "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
+                   "s"(P.norm), "s"(P.B), "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.seed),
+                   "s"(tab.rs.ctr), "s"(P.exi[0]), "s"(P.exi[1]));
+    else
+      asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
+                   "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
+                   "s"(P.norm), "s"(P.B));
+  } else {
+    asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.H), "s"(P.stats), "s"(P.Aout), "s"(P.W), "s"(P.bias),
+                 "s"(P.C), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.ldh), "s"(P.ldao), "s"(P.ldw), "s"(P.Nout),
+                 "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.hot_pad));
+    if constexpr (PRO == kProGather)
+      asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]),
+                   "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
+                   "s"(tab.rs.ctr));
+  }
   const int mtiles = Bp >> 5;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
@@ -1035,6 +1047,10 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
   }
 
+  if constexpr (kL0)         // l0_late_fields: requested behind the operand loads (waited for in their shadow)
+    asm volatile("" ::"s"(P.ex[10]), "s"(P.Aout), "s"(P.ldao), "s"(P.stats), "s"(P.Kreal), "s"(P.C), "s"(P.ldc),
+                 "s"(P.relu), "s"(P.ntiles), "s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.exi[3]),
+                 "s"(P.exi[8]), "s"(tab.rs.idx_out));
   TL_MARK(5);
   // WN >= 2 waves own more chunks than kCh: the next two are requested right behind the A rows
   // (in flight during the LayerNorm, not queued ahead of it), the rest stream in the MFMA loop
