@@ -1535,18 +1535,21 @@ __global__ __launch_bounds__(256, 3) void dw_kernel(DwArgs a, int nb) {
     float a0[16], b0[16], a1[16], b1[16];
     if (cb < ce) dw_load_chunk(P, cb, h, n0, k0, i, a0, b0);
     if (cb + 1 < ce) dw_load_chunk(P, cb + 1, h, n0, k0, i, a1, b1);
-    // the optimizer state of this thread's 4 elements, requested behind the first two operand
-    // chunks (their MFMA waits do not include it) and landing during the MFMA chain
-    int64_t idx[4];
-    bool ok[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = threadIdx.x + 256 * q;
-      idx[q] = P.offW + (int64_t)(n0 + (e >> 5)) * P.Kp + k0 + (e & 31);
-      ok[q] = true;
+    // the optimizer state of this thread's 4 elements (row tn, columns tq..tq+3 of the tile: one
+    // float4 per array, a quarter of the memory instructions of 4 scalar elements), requested
+    // behind the first two operand chunks (their MFMA waits do not include it) and landing during
+    // the MFMA chain.  T is read from a valid address whatever the mode (a `pol ?` select on it
+    // compiled to a branch whose join drained the loads in flight).
+    const int tn = threadIdx.x >> 3, tq = (threadIdx.x & 7) * 4;
+    const int64_t ix = P.offW + (int64_t)(n0 + tn) * P.Kp + k0 + tq;
+    const bool grad_only = a.mode == kDwGrad, pol = a.mode == kDwAdamPolyak;
+    float4 sm4 = make_float4(0.f, 0.f, 0.f, 0.f), sv4 = sm4, sp4 = sm4, st4 = sm4;
+    if (!grad_only) {
+      sm4 = gld4(a.adam.M + ix);
+      sv4 = gld4(a.adam.V + ix);
+      sp4 = gld4(a.adam.P + ix);
+      st4 = gld4((pol ? a.adam.T : a.adam.P) + ix);
     }
-    AdamState<4> st;
-    adam_state_load<4>(a, idx, ok, st);
     for (int rc = cb; rc < ce; rc += 2) {
 #pragma unroll
       for (int s = 0; s < 16; ++s) acc = mfma32x32x2(a0[s], b0[s], acc);
@@ -1566,14 +1569,30 @@ __global__ __launch_bounds__(256, 3) void dw_kernel(DwArgs a, int nb) {
     float gq[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int e = threadIdx.x + 256 * q;
-      const int n = e >> 5, kk = e & 31;
-      float g = red[n * 33 + kk];
+      float g = red[tn * 33 + tq + q];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) g = g + red[(w * 32 + n) * 33 + kk];
+      for (int w = 1; w < 4; ++w) g = g + red[(w * 32 + tn) * 33 + tq + q];
       gq[q] = g;
     }
-    apply_grads_loaded<4>(a, k, idx, gq, ok, st);
+    if (grad_only) {
+      gst4(a.adam.G + ix, make_float4(gq[0], gq[1], gq[2], gq[3]));
+    } else {
+      float mm[4] = {sm4.x, sm4.y, sm4.z, sm4.w}, vv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
+      float pp[4] = {sp4.x, sp4.y, sp4.z, sp4.w}, tt[4] = {st4.x, st4.y, st4.z, st4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {                // torch _single_tensor_adam, as adam_elem
+        mm[e] = __fmaf_rn(k.w1, gq[e] - mm[e], mm[e]);
+        vv[e] = vv[e] * k.b2;
+        vv[e] = vv[e] + (k.c2 * gq[e]) * gq[e];
+        const float denom = sqrtf(vv[e]) / k.bc2s + k.eps;
+        pp[e] = pp[e] + (k.negss * mm[e]) / denom;
+        tt[e] = k.tau * pp[e] + k.omt * tt[e];
+      }
+      gst4(a.adam.M + ix, make_float4(mm[0], mm[1], mm[2], mm[3]));
+      gst4(a.adam.V + ix, make_float4(vv[0], vv[1], vv[2], vv[3]));
+      gst4(a.adam.P + ix, make_float4(pp[0], pp[1], pp[2], pp[3]));
+      if (pol) gst4(a.adam.T + ix, make_float4(tt[0], tt[1], tt[2], tt[3]));
+    }
     TL_MARK(3);
     return;
   }
