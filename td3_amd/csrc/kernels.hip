@@ -1264,12 +1264,16 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 
 // templated on NORM and with the problems in the kernel arguments: a runtime `norm` select on
 // the statistics loads compiled to a branch and a load drain per row (5 dependent load rounds)
+#ifndef TD3_LNBWD_RB
+#define TD3_LNBWD_RB 1
+#endif
+constexpr int kLnBwdRB = TD3_LNBWD_RB;   // rows per wave: 1 (4: 4.0 us per launch, 2: 3.4, 1: 3.2)
 template <bool NORM>
 __global__ __launch_bounds__(256) void lnbwd_rows_kernel(int Bp, LnBwdTable tab) {   // Bp first: preloaded
-  constexpr int RB = 4;
+  constexpr int RB = kLnBwdRB;
   const LnBwdProb& P = tab.p[blockIdx.y];
   const int lane = threadIdx.x & 63;
-  // grid.x = Bp / 16 exactly (Bp is a multiple of 32): no bounds check, which would put a
+  // grid.x = Bp / (4 RB) exactly (Bp is a multiple of 32): no bounds check, which would put a
   // kernel-argument round trip ahead of the table's
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RB;
   float gu[RB][8], h[RB][8], g[8], mean[RB], rstd[RB];
@@ -1816,12 +1820,12 @@ int launch_heads(const HeadArgs& a, int nprob, hipStream_t s) {
 }
 
 int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s) {
-  if (nprob < 1 || nprob > kMaxLnBwd || Bp % 16 != 0) {
-    set_error("launch_lnbwd_rows: %d problems (max %d), Bp %d (multiple of 16)", nprob, kMaxLnBwd, Bp);
+  if (nprob < 1 || nprob > kMaxLnBwd || Bp % (4 * kLnBwdRB) != 0) {
+    set_error("launch_lnbwd_rows: %d problems (max %d), Bp %d (multiple of %d)", nprob, kMaxLnBwd, Bp, 4 * kLnBwdRB);
     return -1;
   }
-  if (norm) hipLaunchKernelGGL(lnbwd_rows_kernel<true>, dim3(Bp / 16, nprob), dim3(256), 0, s, Bp, tab);
-  else hipLaunchKernelGGL(lnbwd_rows_kernel<false>, dim3(Bp / 16, nprob), dim3(256), 0, s, Bp, tab);
+  if (norm) hipLaunchKernelGGL(lnbwd_rows_kernel<true>, dim3(Bp / (4 * kLnBwdRB), nprob), dim3(256), 0, s, Bp, tab);
+  else hipLaunchKernelGGL(lnbwd_rows_kernel<false>, dim3(Bp / (4 * kLnBwdRB), nprob), dim3(256), 0, s, Bp, tab);
   TD3_HIP(hipGetLastError());
   return 0;
 }
