@@ -844,12 +844,16 @@ __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const Ro
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
 }
 
+#ifndef TD3_ROW_WAVES
+#define TD3_ROW_WAVES 1
+#endif
+constexpr int kRowWaves = TD3_ROW_WAVES;   // waves (rows) per row-kernel workgroup: 1 (A/B 4 / 2 / 1: C2 8.93k / 9.03k / 9.09k; the waves of a row stage spread over 4x the CUs, whose load units they no longer share)
 template <int KIND, bool NORM>
-__global__ __launch_bounds__(256) void row_kernel(int Bp, GemmTable tab) {   // Bp first: preloaded
+__global__ __launch_bounds__(64 * kRowWaves) void row_kernel(int Bp, GemmTable tab) {   // Bp first: preloaded
   const GemmProb& P = tab.p[blockIdx.y];
-  // grid.x = Bp / 4 exactly (launch_rows): every wave owns a row, no bounds check (which would put
+  // grid.x = Bp / kRowWaves exactly (launch_rows): every wave owns a row, no bounds check (which would put
   // a kernel-argument round trip ahead of the row's loads)
-  const RowCtx c{(int)(blockIdx.x * 4 + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
+  const RowCtx c{(int)(blockIdx.x * kRowWaves + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
   TL_MARK(0);
   if constexpr (KIND == kRowPolicyHead) row_policy_head<NORM>(P, c);
   else if constexpr (KIND == kRowCriticLoss) row_critic_loss<NORM>(P, c);
@@ -1269,13 +1273,13 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 #endif
 constexpr int kLnBwdRB = TD3_LNBWD_RB;   // rows per wave: 1 (4: 4.0 us per launch, 2: 3.4, 1: 3.2)
 template <bool NORM>
-__global__ __launch_bounds__(256) void lnbwd_rows_kernel(int Bp, LnBwdTable tab) {   // Bp first: preloaded
+__global__ __launch_bounds__(64 * kRowWaves) void lnbwd_rows_kernel(int Bp, LnBwdTable tab) {   // Bp first: preloaded
   constexpr int RB = kLnBwdRB;
   const LnBwdProb& P = tab.p[blockIdx.y];
   const int lane = threadIdx.x & 63;
-  // grid.x = Bp / (4 RB) exactly (Bp is a multiple of 32): no bounds check, which would put a
+  // grid.x = Bp / (kRowWaves RB) exactly (Bp is a multiple of 32): no bounds check, which would put a
   // kernel-argument round trip ahead of the table's
-  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RB;
+  const int row0 = (blockIdx.x * kRowWaves + (threadIdx.x >> 6)) * RB;
   float gu[RB][8], h[RB][8], g[8], mean[RB], rstd[RB];
   float4 qg[2], qu[RB][2], qh[RB][2];
   if constexpr (NORM) rv_load_raw(qg, P.lng, P.ld, lane);
@@ -1781,20 +1785,20 @@ int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int 
 
 template <bool NORM>
 static void launch_rows_t(int kind, const GemmTable& d, int Bp, hipStream_t s) {
-  const dim3 grid(Bp / 4, d.nprob);
+  const dim3 grid(Bp / kRowWaves, d.nprob);
   switch (kind) {
-    case kRowPolicyHead: hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(256), 0, s, Bp, d); break;
-    case kRowCriticLoss: hipLaunchKernelGGL((row_kernel<kRowCriticLoss, NORM>), grid, dim3(256), 0, s, Bp, d); break;
-    case kRowActorLoss: hipLaunchKernelGGL((row_kernel<kRowActorLoss, NORM>), grid, dim3(256), 0, s, Bp, d); break;
+    case kRowPolicyHead: hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
+    case kRowCriticLoss: hipLaunchKernelGGL((row_kernel<kRowCriticLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
+    case kRowActorLoss: hipLaunchKernelGGL((row_kernel<kRowActorLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
     case kRowActorHeadBwd:
-      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(256), 0, s, Bp, d);
+      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
       break;
     case kRowCriticLossP:
-      hipLaunchKernelGGL((row_kernel<kRowCriticLossP, NORM>), grid, dim3(256), 0, s, Bp, d);
+      hipLaunchKernelGGL((row_kernel<kRowCriticLossP, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
       break;
-    case kRowActorLossP: hipLaunchKernelGGL((row_kernel<kRowActorLossP, NORM>), grid, dim3(256), 0, s, Bp, d); break;
+    case kRowActorLossP: hipLaunchKernelGGL((row_kernel<kRowActorLossP, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
     case kRowActorHeadBwdP:
-      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwdP, NORM>), grid, dim3(256), 0, s, Bp, d);
+      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwdP, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
       break;
     default: break;
   }
@@ -1820,12 +1824,12 @@ int launch_heads(const HeadArgs& a, int nprob, hipStream_t s) {
 }
 
 int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s) {
-  if (nprob < 1 || nprob > kMaxLnBwd || Bp % (4 * kLnBwdRB) != 0) {
-    set_error("launch_lnbwd_rows: %d problems (max %d), Bp %d (multiple of %d)", nprob, kMaxLnBwd, Bp, 4 * kLnBwdRB);
+  if (nprob < 1 || nprob > kMaxLnBwd || Bp % (kRowWaves * kLnBwdRB) != 0) {
+    set_error("launch_lnbwd_rows: %d problems (max %d), Bp %d (multiple of %d)", nprob, kMaxLnBwd, Bp, kRowWaves * kLnBwdRB);
     return -1;
   }
-  if (norm) hipLaunchKernelGGL(lnbwd_rows_kernel<true>, dim3(Bp / (4 * kLnBwdRB), nprob), dim3(256), 0, s, Bp, tab);
-  else hipLaunchKernelGGL(lnbwd_rows_kernel<false>, dim3(Bp / (4 * kLnBwdRB), nprob), dim3(256), 0, s, Bp, tab);
+  if (norm) hipLaunchKernelGGL(lnbwd_rows_kernel<true>, dim3(Bp / (kRowWaves * kLnBwdRB), nprob), dim3(64 * kRowWaves), 0, s, Bp, tab);
+  else hipLaunchKernelGGL(lnbwd_rows_kernel<false>, dim3(Bp / (kRowWaves * kLnBwdRB), nprob), dim3(64 * kRowWaves), 0, s, Bp, tab);
   TD3_HIP(hipGetLastError());
   return 0;
 }
