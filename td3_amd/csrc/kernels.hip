@@ -312,26 +312,34 @@ __device__ __forceinline__ void l0_mfma(const GemmProb& P, const float* xs, floa
     av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
   }
   const bool keep = P.ex[10] && P.norm;   // H0 kept in LDS for l0_store_rows (LN overwrites smem)
+  // both tiles' MFMA chains first (two accumulators), then the epilogues, with the uniform `keep`
+  // hoisted out of the element loop (inside it, it compiled to a branch per element)
+  f32x16 acc[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[ct][r] = 0.f;
+    if (c.wave + kNW * ct >= n0t) continue;
+#pragma unroll
+    for (int s = 0; s < 12; ++s) acc[ct] = mfma32x32x2(av[s], w0[ct][s], acc[ct]);
+    if (!k24) {
+#pragma unroll
+      for (int s = 12; s < 16; ++s) acc[ct] = mfma32x32x2(av[s], w0[ct][s], acc[ct]);
+    }
+  }
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     const int tile = c.wave + kNW * ct;
     if (tile >= n0t) continue;
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 12; ++s) acc = mfma32x32x2(av[s], w0[ct][s], acc);
-    if (!k24) {
-#pragma unroll
-      for (int s = 12; s < 16; ++s) acc = mfma32x32x2(av[s], w0[ct][s], acc);
-    }
     const int col = tile * 32 + i;
+    float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = mfma_row(r, c.lane);
-      const float v = fmaxf(acc[r] + b0[ct], 0.f);
-      smem[row * c.S + col] = v;
-      if (keep) h0s[row * c.S + col] = v;
+    for (int r = 0; r < 16; ++r) v[r] = fmaxf(acc[ct][r] + b0[ct], 0.f);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) smem[mfma_row(r, c.lane) * c.S + col] = v[r];
+    if (keep) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) h0s[mfma_row(r, c.lane) * c.S + col] = v[r];
     }
   }
 }
