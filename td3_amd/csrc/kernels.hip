@@ -1467,21 +1467,32 @@ __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P,
   const bool ok[3] = {hasb, ln, ln};
   AdamState<3> st;
   float sb[4] = {0.f, 0.f, 0.f, 0.f}, sg[4] = {0.f, 0.f, 0.f, 0.f}, sbeta[4] = {0.f, 0.f, 0.f, 0.f};
+  // every operand read unconditionally from a valid address (the bias-less / LN-less operands
+  // alias a present one) and masked at use: `hasb ?` / `if (ln)` on the loads compiled to
+  // branches whose joins drained the loads in flight
+  const float* gzp = hasb ? P.G : P.GU;
+  const float* gup = ln ? P.GU : P.G;
+  const float* hp = ln ? P.H : P.G;
+  const float* stp = ln ? P.stats : P.G;
+  const int ldz = hasb ? P.ldg : P.ldgu, ldu = ln ? P.ldgu : P.ldg, ldh = ln ? P.ldh : P.ldg;
   for (int r0 = rg; r0 < a.Bp; r0 += RG * U) {
     float4 gz[U], gu[U], hh[U];
     float mu[U], rs[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = min(r0 + RG * u, a.Bp - 1);     // clamped: loads stay unconditional
-      gz[u] = hasb ? gld4(P.G + ((size_t)r * P.ldg + n0 + c4)) : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ln) {
-        gu[u] = gld4(P.GU + ((size_t)r * P.ldgu + n0 + c4));
-        hh[u] = gld4(P.H + ((size_t)r * P.ldh + n0 + c4));
-        mu[u] = gld(P.stats + r);
-        rs[u] = gld(P.stats + (a.Bp + r));
-      }
+      gz[u] = gld4(gzp + ((size_t)r * ldz + n0 + c4));
+      gu[u] = gld4(gup + ((size_t)r * ldu + n0 + c4));
+      hh[u] = gld4(hp + ((size_t)r * ldh + n0 + c4));
+      mu[u] = gld(stp + r);
+      rs[u] = gld(stp + (a.Bp + r));
     }
     if (r0 == rg && threadIdx.x < 32) adam_state_load<3>(a, idx, ok, st);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!hasb) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) gz[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (r0 + RG * u >= a.Bp) continue;
