@@ -1536,7 +1536,10 @@ __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P,
 // 4 waves, operands of the next row chunk in flight while the current one is multiplied).
 // Vector tiles: db = sum dZ, dgamma = sum dU*xhat, dbeta = sum dU over 32 columns.
 // Both end in the fused optimizer update of the elements they own.
-__global__ __launch_bounds__(256, 3) void dw_kernel(DwArgs a, int nb) {
+#ifndef TD3_DW_OCC
+#define TD3_DW_OCC 3
+#endif
+__global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
   __shared__ float red[4 * 32 * 33];
   const int b = xcd_tile(nb);
   TL_MARK(0);
