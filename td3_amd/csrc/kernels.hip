@@ -952,6 +952,9 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 // first and is preloaded into SGPRs at wave launch (-amdgpu-kernarg-preload-count, build.py), so
 // the problem select costs no memory round trip; the problem's fields are then the first and only
 // kernel-argument round trip ahead of the operand loads.
+#ifndef TD3_L0G_LATE_B
+#define TD3_L0G_LATE_B 1
+#endif
 template <int MODE, int WN, int PRO>
 __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
                                                         GemmTable tab, Counters* bump, int bump_actor) {
@@ -1053,7 +1056,10 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
       rv_load(lb, P.lnb, P.Kp, lane);
     }
   }
-  if constexpr (kPrefetchB) {
+  // the sampled-record stage (kProL0G) requests its layer-1 weights after the records landed:
+  // in flight together, they delayed the latency-critical random record reads
+  constexpr bool kLateB = PRO == kProL0G && TD3_L0G_LATE_B;
+  if constexpr (kPrefetchB && !kLateB) {
     if constexpr (WN == 0) load_b16<MODE, kCh>(P, bv, cb, nch, ncol, lane >> 4);
     else load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
     __builtin_amdgcn_sched_barrier(0);     // keep the weight requests ahead of the prologue
@@ -1084,6 +1090,10 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   else if constexpr (kL0) {
     float* xs = smem + 32 * S;
     l0_put_x<PRO == kProL0G>(P, tab.rs, xs, c, pi, l0x);
+    if constexpr (kLateB) {
+      load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     __syncthreads();
     TL_MARK(6);
     l0_mfma(P, xs, smem, xs + 32 * kL0XS, c, w0, b0v);
