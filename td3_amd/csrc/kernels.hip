@@ -955,6 +955,9 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 #ifndef TD3_L0G_LATE_B
 #define TD3_L0G_LATE_B 1
 #endif
+#ifndef TD3_L0_LATE_B
+#define TD3_L0_LATE_B 0
+#endif
 template <int MODE, int WN, int PRO>
 __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
                                                         GemmTable tab, Counters* bump, int bump_actor) {
@@ -1058,7 +1061,7 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   }
   // the sampled-record stage (kProL0G) requests its layer-1 weights after the records landed:
   // in flight together, they delayed the latency-critical random record reads
-  constexpr bool kLateB = PRO == kProL0G && TD3_L0G_LATE_B;
+  constexpr bool kLateB = (PRO == kProL0G && TD3_L0G_LATE_B) || (PRO == kProL0 && TD3_L0_LATE_B);
   if constexpr (kPrefetchB && !kLateB) {
     if constexpr (WN == 0) load_b16<MODE, kCh>(P, bv, cb, nch, ncol, lane >> 4);
     else load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
@@ -1091,7 +1094,8 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
     float* xs = smem + 32 * S;
     l0_put_x<PRO == kProL0G>(P, tab.rs, xs, c, pi, l0x);
     if constexpr (kLateB) {
-      load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
+      if constexpr (WN == 0) load_b16<MODE, kCh>(P, bv, cb, nch, ncol, lane >> 4);
+      else load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
