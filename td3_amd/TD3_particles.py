@@ -197,9 +197,12 @@ class TD3(_FeaturedTD3):
             torch = _torch()
             batch = replay_buffer.sample(B)
             ts = [torch.as_tensor(x, dtype=torch.float32).to(self.device).contiguous() for x in batch]
-            with self._torch_order() as ls:          # the batch was produced on torch's stream
-                for t in ts:
-                    t.record_stream(ls)
+            # the batch was produced on torch's stream; on exit torch's stream waits for the
+            # library's, so the blocks freed with `ts` are reused only after the step read them
+            # (no record_stream: its free-time event on the library stream could outlive the
+            # handle's stream, and a later stream created at the same address made torch's next
+            # allocation fail with hipErrorCapturedEvent)
+            with self._torch_order():
                 check(self._lib.td3_train_step_batch_particles(
                     self._h, *[t.data_ptr() for t in ts], B, self._stream(),
                     _lib.fptr(nz) if nz is not None else None, C.byref(st) if st is not None else None),
