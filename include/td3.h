@@ -145,6 +145,11 @@ int td3_set_params(td3_handle* h, int which, const float* in, int64_t n);
 int td3_get_counters(const td3_handle* h, int64_t* total_it, int64_t* critic_step,
                      int64_t* actor_step);
 int td3_set_counters(td3_handle* h, int64_t total_it, int64_t critic_step, int64_t actor_step);
+/* Adam hyper-parameters of one optimizer (group 0 actor, 1 critic): torch.optim.Adam's
+ * param_groups[0] lr / betas / eps, which Adam.load_state_dict adopts from a checkpoint
+ * (TD3_base.py:37-50 loads actor_optimizer / critic_optimizer).  Synchronises the learner. */
+int td3_set_adam(td3_handle* h, int group, double lr, double beta1, double beta2, double eps);
+int td3_get_adam(const td3_handle* h, int group, double out[4] /* lr, beta1, beta2, eps */);
 
 /* One TD3.train(rb, batch) step.  inject_idx [batch] int64 / inject_noise [batch][ad]
  * float32 are HOST arrays (nullable) replacing the Philox draws (parity testing).

@@ -120,8 +120,8 @@ class _AdamView:
             for i, k in enumerate(m):
                 state[i] = {"step": torch.tensor(float(step)), "exp_avg": torch.from_numpy(m[k]),
                             "exp_avg_sq": torch.from_numpy(v[k])}
-        cfg = self._o._cfg
-        group = {"lr": cfg.lr, "betas": (cfg.beta1, cfg.beta2), "eps": cfg.eps, "weight_decay": 0,
+        lr, b1, b2, eps = self._o._adam_hparams(self._group)
+        group = {"lr": lr, "betas": (b1, b2), "eps": eps, "weight_decay": 0,
                  "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
                  "differentiable": False, "fused": None, "decoupled_weight_decay": False,
                  "params": list(range(len(m)))}
@@ -150,7 +150,7 @@ class _AdamView:
             self._o._set_counters(t, step, as_)
         pg = sd.get("param_groups")
         if pg:
-            self._o._lr_from_group(pg[0])
+            self._o._adam_from_group(self._group, pg[0])
 
     def zero_grad(self, set_to_none=True):
         pass
@@ -249,9 +249,22 @@ class TD3(TD3_base):
     def _set_counters(self, t, c, a):
         check(self._lib.td3_set_counters(self._h, int(t), int(c), int(a)), "td3_set_counters")
 
-    def _lr_from_group(self, group):
-        if abs(float(group.get("lr", self._cfg.lr)) - self._cfg.lr) > 0:
-            raise ValueError("loading an optimizer with a different lr is not supported")
+    def _adam_hparams(self, group):
+        out = (C.c_double * 4)()
+        check(self._lib.td3_get_adam(self._h, group, out), "td3_get_adam")
+        return float(out[0]), float(out[1]), float(out[2]), float(out[3])
+
+    def _adam_from_group(self, group, pg):
+        """Adopt a checkpoint's param_groups[0] as torch.optim.Adam.load_state_dict does
+        (lr / betas / eps); the options the reference never sets must keep torch's defaults."""
+        for k, default in (("weight_decay", 0), ("amsgrad", False), ("maximize", False)):
+            if pg.get(k, default) != default:
+                raise ValueError(f"Adam {k}={pg[k]!r} is not supported (the reference uses the default)")
+        lr, b1, b2, eps = self._adam_hparams(group)
+        lr = float(pg.get("lr", lr))
+        b1, b2 = (float(b) for b in pg.get("betas", (b1, b2)))
+        eps = float(pg.get("eps", eps))
+        check(self._lib.td3_set_adam(self._h, group, lr, b1, b2, eps), "td3_set_adam")
 
     def _stream(self):
         return None                      # the learner's own stream

@@ -71,6 +71,8 @@ SIGNATURES = {
     "td3_set_params": (C.c_int, [_P, C.c_int, _F, C.c_int64]),
     "td3_get_counters": (C.c_int, [_P, _I64, _I64, _I64]),
     "td3_set_counters": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64]),
+    "td3_set_adam": (C.c_int, [_P, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double]),
+    "td3_get_adam": (C.c_int, [_P, C.c_int, _D]),
     "td3_train_step": (C.c_int, [_P, _P, C.c_int, _P, _I64, _F, C.POINTER(td3_step_stats)]),
     "td3_train_step_batch": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_int, _P, _F,
                                        C.POINTER(td3_step_stats)]),

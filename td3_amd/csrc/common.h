@@ -27,6 +27,12 @@ void set_error(const char* fmt, ...);
     }                                                                              \
   } while (0)
 
+#define TD3_RC(expr)          \
+  do {                        \
+    int _rc = (expr);         \
+    if (_rc) return _rc;      \
+  } while (0)
+
 namespace td3 {
 
 constexpr int kWave = 64;
@@ -121,7 +127,7 @@ struct Counters {
   // products by the step bump so no workgroup evaluates pow(): [0] beta1^critic_step,
   // [1] beta2^critic_step, [2] beta1^actor_step, [3] beta2^actor_step
   double pw[4];
-  double beta1, beta2;
+  double beta[4];       // the factor of each pw[] (critic beta1, beta2, actor beta1, beta2)
 };
 
 }  // namespace td3

@@ -1240,12 +1240,12 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     bump->total_it += 1;
     bump->critic_step += 1;
-    bump->pw[0] *= bump->beta1;
-    bump->pw[1] *= bump->beta2;
+    bump->pw[0] *= bump->beta[0];
+    bump->pw[1] *= bump->beta[1];
     if (bump_actor) {
       bump->actor_step += 1;
-      bump->pw[2] *= bump->beta1;
-      bump->pw[3] *= bump->beta2;
+      bump->pw[2] *= bump->beta[2];
+      bump->pw[3] *= bump->beta[3];
     }
   }
 }

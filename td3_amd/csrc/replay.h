@@ -13,6 +13,7 @@ namespace td3 {
 //     reward | not_done | pad ]
 // with sd = F, ad = A; the learner's encoder reads the particle blocks in place (no gather).
 struct Ring {
+  uint64_t gen = 0;                // unique per allocation: captured graphs bake this ring in
   int sd = 0, ad = 0;
   int rec = 0;
   int o_s = 0, o_a = 0, o_s2 = 0, o_r = 0, o_nd = 0;
@@ -26,12 +27,25 @@ struct Ring {
   uint64_t sample_calls = 0;       // Philox counter of the stand-alone sample()
   int device = 0;
   hipStream_t stream = nullptr;
-  float* stage = nullptr;          // pinned host staging for add()
-  size_t stage_cap = 0;
-  hipEvent_t stage_ev = nullptr;
+  float* stage[2] = {nullptr, nullptr};     // pinned host staging for add(), double-buffered
+  size_t stage_cap[2] = {0, 0};
+  hipEvent_t stage_buf_ev[2] = {nullptr, nullptr};  // H2D out of stage[i] finished
+  int stage_cur = 0;
+  hipEvent_t stage_ev = nullptr;   // the last write (records + d_size): readers wait on it
+  // Ordering of writes after reads.  Every reader (a learner step, a stand-alone sample) records
+  // read_ev on its stream after the work that reads the records or d_size; a later write waits on
+  // it, so a step in flight never sees d_size or a record change under it.  Readers on different
+  // streams are chained (the new reader waits on read_ev first), so read_ev covers them all.
+  hipEvent_t read_ev = nullptr;
+  const void* read_stream = nullptr;        // stream of the last read_ev record (compared only)
   int64_t* d_idx = nullptr;        // last drawn indices (rows) of sample()
   int idx_cap = 0;
 };
+
+// Reader protocol (see Ring::read_ev): ring_begin_read before enqueuing reads on s (waits on
+// the last write and, on a new stream, on the previous readers), ring_end_read after them.
+int ring_begin_read(Ring* r, hipStream_t s);
+int ring_end_read(Ring* r, hipStream_t s);
 
 // One gather destination: rows [0, Bp) of dst[r*ld + col + c] = record[src + c], c < len.
 struct GatherSeg {

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <atomic>
 
 #include "replay.h"
 #include "../../include/td3.h"
@@ -110,6 +111,18 @@ __global__ __launch_bounds__(256) void fill_kernel(float* data, int rec, int o_a
 
 __global__ void set_i64_kernel(int64_t* p, int64_t v) { *p = v; }
 
+int ring_begin_read(Ring* r, hipStream_t s) {
+  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
+  if (r->read_stream && r->read_stream != (const void*)s) TD3_HIP(hipStreamWaitEvent(s, r->read_ev, 0));
+  return 0;
+}
+
+int ring_end_read(Ring* r, hipStream_t s) {
+  TD3_HIP(hipEventRecord(r->read_ev, s));
+  r->read_stream = s;
+  return 0;
+}
+
 }  // namespace td3
 
 using namespace td3;
@@ -117,7 +130,10 @@ using namespace td3;
 // ================================================================== C-ABI
 extern "C" {
 
+static std::atomic<uint64_t> g_ring_gen{0};
+
 static int ring_alloc(Ring* r, int64_t max_size, int device, uint64_t seed, rb_handle** out) {
+  r->gen = ++g_ring_gen;
   r->cap = max_size;
   r->seed = seed;
   r->device = device;
@@ -136,6 +152,8 @@ static int ring_alloc(Ring* r, int64_t max_size, int device, uint64_t seed, rb_h
   TD3_HIP(hipDeviceSynchronize());
   TD3_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
   TD3_HIP(hipEventCreateWithFlags(&r->stage_ev, hipEventDisableTiming));
+  TD3_HIP(hipEventCreateWithFlags(&r->read_ev, hipEventDisableTiming));
+  for (auto& ev : r->stage_buf_ev) TD3_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   *out = reinterpret_cast<rb_handle*>(r);
   return 0;
 }
@@ -188,11 +206,17 @@ int rb_destroy(rb_handle* h) {
   Ring* r = reinterpret_cast<Ring*>(h);
   (void)hipSetDevice(r->device);
   (void)hipStreamSynchronize(r->stream);
+  if (r->read_stream) (void)hipEventSynchronize(r->read_ev);   // no reader still in flight
   (void)hipFree(r->data);
   (void)hipFree(r->d_size);
   (void)hipFree(r->d_idx);
-  if (r->stage) (void)hipHostFree(r->stage);
+  for (int i = 0; i < 2; ++i) {
+    if (r->stage_buf_ev[i]) (void)hipEventSynchronize(r->stage_buf_ev[i]);
+    if (r->stage[i]) (void)hipHostFree(r->stage[i]);
+    (void)hipEventDestroy(r->stage_buf_ev[i]);
+  }
   (void)hipEventDestroy(r->stage_ev);
+  (void)hipEventDestroy(r->read_ev);
   (void)hipStreamDestroy(r->stream);
   delete r;
   return 0;
@@ -216,34 +240,63 @@ int rb_info(const rb_handle* h, rb_info_t* info) {
   return 0;
 }
 
-static int ensure_stage(Ring* r, size_t floats) {
-  if (floats <= r->stage_cap) {
-    TD3_HIP(hipEventSynchronize(r->stage_ev));   // previous async H2D has consumed it
-    return 0;
+// Pinned staging for the next add: alternate between two buffers so the host packs the next
+// rows while the previous upload (which may be waiting behind a step that reads the ring) is
+// still queued; only the upload before that one must have consumed its buffer.
+static float* ensure_stage(Ring* r, size_t floats) {
+  const int i = r->stage_cur;
+  r->stage_cur ^= 1;
+  if (hipEventSynchronize(r->stage_buf_ev[i]) != hipSuccess) return nullptr;
+  if (floats > r->stage_cap[i]) {
+    if (r->stage[i]) (void)hipHostFree(r->stage[i]);
+    r->stage[i] = nullptr;
+    r->stage_cap[i] = 0;
+    const size_t cap = std::max(floats, (size_t)r->rec * 4096);
+    hipError_t e = hipHostMalloc(&r->stage[i], cap * sizeof(float), hipHostMallocDefault);
+    if (e != hipSuccess) {
+      set_error("rb_add: hipHostMalloc(%zu bytes) failed: %s", cap * sizeof(float), hipGetErrorString(e));
+      return nullptr;
+    }
+    r->stage_cap[i] = cap;
   }
-  TD3_HIP(hipEventSynchronize(r->stage_ev));
-  if (r->stage) TD3_HIP(hipHostFree(r->stage));
-  size_t cap = std::max(floats, (size_t)r->rec * 4096);
-  TD3_HIP(hipHostMalloc(&r->stage, cap * sizeof(float), hipHostMallocDefault));
-  r->stage_cap = cap;
+  return r->stage[i];
+}
+
+static hipEvent_t stage_event_of(Ring* r, const float* host) {
+  for (int i = 0; i < 2; ++i)
+    if (host == r->stage[i]) return r->stage_buf_ev[i];
+  return nullptr;
+}
+
+// Writes (records, d_size) on `stream` start after every read queued so far (Ring::read_ev).
+static int ring_begin_write(Ring* r, hipStream_t stream) {
+  if (r->read_stream && r->read_stream != (const void*)stream)
+    TD3_HIP(hipStreamWaitEvent(stream, r->read_ev, 0));
+  return 0;
+}
+
+static int ring_end_write(Ring* r, hipStream_t stream) {
+  TD3_HIP(hipEventRecord(r->stage_ev, stream));
   return 0;
 }
 
 // Copy n packed records (host staging) into the ring at ptr, wrapping (the ring
 // semantics of my_replay_buffer.py:115-116 applied n times).
 static int push_staged(Ring* r, const float* host, int64_t n, hipStream_t stream) {
+  TD3_RC(ring_begin_write(r, stream));
   int64_t done = 0;
   // Only the last `cap` records survive when n > cap.
+  const float* src = host;
   if (n > r->cap) {
     int64_t skip = n - r->cap;
     r->ptr = (r->ptr + skip) % r->cap;
-    host += (size_t)skip * r->rec;
+    src += (size_t)skip * r->rec;
     n = r->cap;
     r->size = r->cap;
   }
   while (done < n) {
     int64_t chunk = std::min<int64_t>(n - done, r->cap - r->ptr);
-    TD3_HIP(hipMemcpyAsync(r->data + (size_t)r->ptr * r->rec, host + (size_t)done * r->rec,
+    TD3_HIP(hipMemcpyAsync(r->data + (size_t)r->ptr * r->rec, src + (size_t)done * r->rec,
                            (size_t)chunk * r->rec * sizeof(float), hipMemcpyHostToDevice, stream));
     r->ptr = (r->ptr + chunk) % r->cap;
     done += chunk;
@@ -251,8 +304,8 @@ static int push_staged(Ring* r, const float* host, int64_t n, hipStream_t stream
   r->size = std::min<int64_t>(r->size + n, r->cap);
   hipLaunchKernelGGL(set_i64_kernel, dim3(1), dim3(1), 0, stream, r->d_size, r->size);
   TD3_HIP(hipGetLastError());
-  TD3_HIP(hipEventRecord(r->stage_ev, stream));
-  return 0;
+  if (hipEvent_t be = stage_event_of(r, host)) TD3_HIP(hipEventRecord(be, stream));
+  return ring_end_write(r, stream);
 }
 
 int rb_add(rb_handle* h, const double* state, const double* action, const double* next_state,
@@ -264,10 +317,10 @@ int rb_add(rb_handle* h, const double* state, const double* action, const double
   Ring* r = reinterpret_cast<Ring*>(h);
   TD3_ARG(!r->particles, "rb_add on a particle ring (use rb_add_particles)");
   TD3_HIP(hipSetDevice(r->device));
-  int rc = ensure_stage(r, (size_t)n * r->rec);
-  if (rc) return rc;
+  float* stage = ensure_stage(r, (size_t)n * r->rec);
+  if (!stage) return -2;
   for (int64_t i = 0; i < n; ++i) {
-    float* d = r->stage + (size_t)i * r->rec;
+    float* d = stage + (size_t)i * r->rec;
     for (int c = 0; c < r->sd; ++c) d[r->o_s + c] = (float)state[i * r->sd + c];
     for (int c = 0; c < r->ad; ++c) d[r->o_a + c] = (float)action[i * r->ad + c];
     for (int c = 0; c < r->sd; ++c) d[r->o_s2 + c] = (float)next_state[i * r->sd + c];
@@ -276,7 +329,7 @@ int rb_add(rb_handle* h, const double* state, const double* action, const double
     for (int c = r->o_nd + 1; c < r->rec; ++c) d[c] = 0.f;
   }
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
-  return push_staged(r, r->stage, n, s);
+  return push_staged(r, stage, n, s);
 }
 
 int rb_add_particles(rb_handle* h, const double* feat, const double* part, const double* action,
@@ -289,11 +342,11 @@ int rb_add_particles(rb_handle* h, const double* feat, const double* part, const
   Ring* r = reinterpret_cast<Ring*>(h);
   TD3_ARG(r->particles, "rb_add_particles on a featured ring");
   TD3_HIP(hipSetDevice(r->device));
-  int rc = ensure_stage(r, (size_t)n * r->rec);
-  if (rc) return rc;
+  float* stage = ensure_stage(r, (size_t)n * r->rec);
+  if (!stage) return -2;
   const int np = r->N * r->D;
   for (int64_t i = 0; i < n; ++i) {                        // my_replay_buffer.py:46-56
-    float* d = r->stage + (size_t)i * r->rec;
+    float* d = stage + (size_t)i * r->rec;
     for (int c = 0; c < r->sd; ++c) d[r->o_s + c] = (float)feat[i * r->sd + c];
     for (int c = 0; c < np; ++c) d[r->o_p + c] = (float)part[i * np + c];
     for (int c = 0; c < r->ad; ++c) d[r->o_a + c] = (float)action[i * r->ad + c];
@@ -304,7 +357,7 @@ int rb_add_particles(rb_handle* h, const double* feat, const double* part, const
     for (int c = r->o_nd + 1; c < r->rec; ++c) d[c] = 0.f;
   }
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
-  return push_staged(r, r->stage, n, s);
+  return push_staged(r, stage, n, s);
 }
 
 int rb_add_records(rb_handle* h, const float* records, int64_t n, void* stream) {
@@ -314,11 +367,11 @@ int rb_add_records(rb_handle* h, const float* records, int64_t n, void* stream) 
   TD3_ARG(records != nullptr, "null records");
   Ring* r = reinterpret_cast<Ring*>(h);
   TD3_HIP(hipSetDevice(r->device));
-  int rc = ensure_stage(r, (size_t)n * r->rec);
-  if (rc) return rc;
-  memcpy(r->stage, records, (size_t)n * r->rec * sizeof(float));
+  float* stage = ensure_stage(r, (size_t)n * r->rec);
+  if (!stage) return -2;
+  memcpy(stage, records, (size_t)n * r->rec * sizeof(float));
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
-  return push_staged(r, r->stage, n, s);
+  return push_staged(r, stage, n, s);
 }
 
 int rb_fill_synthetic(rb_handle* h, int64_t n, float max_action, uint64_t seed, void* stream) {
@@ -328,6 +381,7 @@ int rb_fill_synthetic(rb_handle* h, int64_t n, float max_action, uint64_t seed, 
   TD3_HIP(hipSetDevice(r->device));
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
   if (n > r->cap) n = r->cap;
+  TD3_RC(ring_begin_write(r, s));
   if (n > 0) {
     dim3 grid((unsigned)((n + 3) / 4));
     hipLaunchKernelGGL(fill_kernel, grid, dim3(256), 0, s, r->data, r->rec, r->o_a, r->ad, r->o_r, r->o_nd,
@@ -338,8 +392,7 @@ int rb_fill_synthetic(rb_handle* h, int64_t n, float max_action, uint64_t seed, 
   r->size = std::min<int64_t>(r->size + n, r->cap);
   hipLaunchKernelGGL(set_i64_kernel, dim3(1), dim3(1), 0, s, r->d_size, r->size);
   TD3_HIP(hipGetLastError());
-  TD3_HIP(hipEventRecord(r->stage_ev, s));
-  return 0;
+  return ring_end_write(r, s);
 }
 
 int rb_sample(rb_handle* h, int batch, float* state, float* action, float* next_state,
@@ -369,8 +422,9 @@ int rb_sample(rb_handle* h, int batch, float* state, float* action, float* next_
   a.ctr = nullptr;
   a.step = ++r->sample_calls;
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
-  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));   // add() before sample() (main.py:261, :269)
-  return launch_gather(a, s);
+  TD3_RC(ring_begin_read(r, s));                     // add() before sample() (main.py:261, :269)
+  TD3_RC(launch_gather(a, s));
+  return ring_end_read(r, s);
 }
 
 int rb_sample_particles(rb_handle* h, int batch, float* feat, float* part, float* action, float* next_feat,
@@ -403,8 +457,9 @@ int rb_sample_particles(rb_handle* h, int batch, float* feat, float* part, float
   a.ctr = nullptr;
   a.step = ++r->sample_calls;
   hipStream_t s = stream ? (hipStream_t)stream : r->stream;
-  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
-  return launch_gather(a, s);
+  TD3_RC(ring_begin_read(r, s));                     // add() before sample() (main.py:261, :269)
+  TD3_RC(launch_gather(a, s));
+  return ring_end_read(r, s);
 }
 
 int rb_read_records(const rb_handle* h, int64_t start, int64_t n, float* out) {

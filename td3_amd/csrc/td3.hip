@@ -42,12 +42,6 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-#define TD3_RC(expr)          \
-  do {                        \
-    int _rc = (expr);         \
-    if (_rc) return _rc;      \
-  } while (0)
-
 // ------------------------------------------------------------------ layouts
 struct LinearL { int N, K, Np, Kp; int64_t offW, offb; };
 struct LNormL { int N, Np; int64_t offg, offb; };
@@ -192,7 +186,7 @@ struct Plan {
   hipGraphExec_t graph[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   // the same bodies with the replay-ring gather captured in front (Philox draw path)
   hipGraphExec_t graph_g[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-  const void* graph_ring = nullptr;
+  uint64_t graph_ring_gen = 0;          // Ring::gen the graph_g variants were captured with
   // ---- TD3_particles
   int particles = 0;
   int nq = 1, ldq = 1;                  // Q outputs per row and the row stride of Y / Qv
@@ -203,7 +197,7 @@ struct Plan {
   const float* src_data = nullptr;      // where the encoders read particles: ring or pbatch
   int src_rec = 0, src_op = 0, src_op2 = 0;
   const int64_t* src_idx = nullptr;
-  const void* src_key = nullptr;
+  uint64_t src_key = 0;                 // Ring::gen of the source ring, kBatchSource for pbatch
   int nwg = 0;                          // encoder-backward workgroups per role per critic network
   int nwg_a = 0;                        // ... for the actor's encoder (one network per launch)
 };
@@ -231,6 +225,10 @@ struct td3_handle {
   float* arena = nullptr;
   Counters* d_ctr = nullptr;
   int64_t total_it = 0, critic_step = 0, actor_step = 0;   // host mirror
+  // Adam hyper-parameters per optimizer, [0] critic, [1] actor (AdamArgs::which).  Both start
+  // from the config; torch's Adam.load_state_dict adopts a checkpoint's param_groups, and so
+  // does td3_set_adam.
+  struct AdamHp { double lr, beta1, beta2, eps; } adam[2];
   hipStream_t stream = nullptr;
   // Acting path: select_action runs on its own stream and waits only for the
   // last step that changed the online actor, so on critic-only steps (total_it % policy_freq != 0)
@@ -660,10 +658,10 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.adam.T = g.T;
   a.adam.ctr = h->d_ctr;
   a.adam.which = which;
-  a.adam.lr = h->cfg.lr;
-  a.adam.beta1 = h->cfg.beta1;
-  a.adam.beta2 = h->cfg.beta2;
-  a.adam.eps = h->cfg.eps;
+  a.adam.lr = h->adam[which].lr;
+  a.adam.beta1 = h->adam[which].beta1;
+  a.adam.beta2 = h->adam[which].beta2;
+  a.adam.eps = h->adam[which].eps;
   a.adam.tau = (float)h->cfg.tau;
   a.adam.grad_scale = 1.0f;
   const bool dp = h->comm != nullptr;
@@ -1069,11 +1067,13 @@ static void destroy_graphs(Plan* P) {
       if (P->graph_g[a][b]) (void)hipGraphExecDestroy(P->graph_g[a][b]);
       P->graph[a][b] = P->graph_g[a][b] = nullptr;
     }
-  P->graph_ring = nullptr;
+  P->graph_ring_gen = 0;
 }
 
 // The encoders read particles in place; graphs bake the source, so a new source re-captures.
-static void set_particle_source(Plan* P, const void* key, const float* data, int rec, int op, int op2,
+constexpr uint64_t kBatchSource = ~0ull;
+
+static void set_particle_source(Plan* P, uint64_t key, const float* data, int rec, int op, int op2,
                                 const int64_t* idx) {
   if (P->src_key == key && P->src_data == data) return;
   destroy_graphs(P);
@@ -1458,14 +1458,16 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
     if (ring && !fused) TD3_RC(input_from_ring(h, ring, P, false, s));
     return run_stages(st, s);
   }
-  if (ring && P->graph_ring != ring) {          // graphs bake the ring's pointers in
+  // graphs bake the ring in (records, d_size, seed, record width): a ring allocated since —
+  // even at the same address, e.g. after ReplayBuffer.load() — is captured again
+  if (ring && P->graph_ring_gen != ring->gen) {
     for (int a = 0; a < 2; ++a)
       for (int b = 0; b < 2; ++b)
         if (P->graph_g[a][b]) {
           TD3_HIP(hipGraphExecDestroy(P->graph_g[a][b]));
           P->graph_g[a][b] = nullptr;
         }
-    P->graph_ring = ring;
+    P->graph_ring_gen = ring->gen;
   }
   hipGraphExec_t& ge = ring ? P->graph_g[actor_phase][inj] : P->graph[actor_phase][inj];
   if (!ge) {
@@ -1508,7 +1510,7 @@ static int ensure_plan(td3_handle* h, int B) {
 static int bind_ring(td3_handle* h, Ring* r) {
   Plan* P = h->plan.get();
   if (P->particles) {
-    set_particle_source(P, r, r->data, r->rec, r->o_p, r->o_p2, P->d_idx);
+    set_particle_source(P, r->gen, r->data, r->rec, r->o_p, r->o_p2, P->d_idx);
     return 0;
   }
   const int sd = h->sd, ad = h->ad;
@@ -1804,12 +1806,14 @@ static Counters make_counters(const td3_handle* h, int64_t total_it, int64_t cri
   c.total_it = total_it;
   c.critic_step = critic_step;
   c.actor_step = actor_step;
-  c.beta1 = h->cfg.beta1;
-  c.beta2 = h->cfg.beta2;
-  c.pw[0] = std::pow(c.beta1, (double)critic_step);
-  c.pw[1] = std::pow(c.beta2, (double)critic_step);
-  c.pw[2] = std::pow(c.beta1, (double)actor_step);
-  c.pw[3] = std::pow(c.beta2, (double)actor_step);
+  c.beta[0] = h->adam[0].beta1;
+  c.beta[1] = h->adam[0].beta2;
+  c.beta[2] = h->adam[1].beta1;
+  c.beta[3] = h->adam[1].beta2;
+  c.pw[0] = std::pow(c.beta[0], (double)critic_step);
+  c.pw[1] = std::pow(c.beta[1], (double)critic_step);
+  c.pw[2] = std::pow(c.beta[2], (double)actor_step);
+  c.pw[3] = std::pow(c.beta[3], (double)actor_step);
   return c;
 }
 
@@ -1833,6 +1837,7 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_RC(encoder_init());
   td3_handle* h = new td3_handle();
   h->cfg = *cfg;
+  h->adam[0] = h->adam[1] = td3_handle::AdamHp{cfg->lr, cfg->beta1, cfg->beta2, cfg->eps};
   h->sd = cfg->state_dim;
   h->ad = cfg->action_dim;
   const bool norm = cfg->norm != 0;
@@ -2020,6 +2025,33 @@ int td3_set_counters(td3_handle* h, int64_t total_it, int64_t critic_step, int64
   return 0;
 }
 
+int td3_set_adam(td3_handle* h, int group, double lr, double beta1, double beta2, double eps) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(group == 0 || group == 1, "group must be 0 (actor) or 1 (critic)");
+  TD3_ARG(lr >= 0 && eps >= 0 && beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1,
+          "Adam hyper-parameters out of range (torch adam.py: 0 <= lr, eps; 0 <= betas < 1)");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_HIP(hipStreamSynchronize(h->stream));
+  td3_handle::AdamHp& hp = h->adam[group == 0 ? 1 : 0];
+  if (hp.lr == lr && hp.beta1 == beta1 && hp.beta2 == beta2 && hp.eps == eps) return 0;
+  hp = td3_handle::AdamHp{lr, beta1, beta2, eps};
+  const Counters c = make_counters(h, h->total_it, h->critic_step, h->actor_step);
+  TD3_HIP(hipMemcpy(h->d_ctr, &c, sizeof(c), hipMemcpyHostToDevice));
+  if (h->plan) TD3_RC(build_plan(h, h->plan->B));   // the dW stages carry lr / betas / eps
+  return 0;
+}
+
+int td3_get_adam(const td3_handle* h, int group, double out[4]) {
+  TD3_ARG(h && out, "null argument");
+  TD3_ARG(group == 0 || group == 1, "group must be 0 (actor) or 1 (critic)");
+  const td3_handle::AdamHp& hp = h->adam[group == 0 ? 1 : 0];
+  out[0] = hp.lr;
+  out[1] = hp.beta1;
+  out[2] = hp.beta2;
+  out[3] = hp.eps;
+  return 0;
+}
+
 int td3_train_step(td3_handle* h, rb_handle* rbh, int batch, void* stream, const int64_t* inject_idx,
                    const float* inject_noise, td3_step_stats* stats) {
   TD3_ARG(h && rbh, "null handle");
@@ -2035,7 +2067,7 @@ int td3_train_step(td3_handle* h, rb_handle* rbh, int batch, void* stream, const
   Plan* P = h->plan.get();
   TD3_RC(bind_ring(h, r));
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
+  TD3_RC(ring_begin_read(r, s));                 // the adds queued before this step, not after
   if (inject_idx) {
     for (int i = 0; i < batch; ++i)
       TD3_ARG(inject_idx[i] >= 0 && inject_idx[i] < r->cap, "injected index out of range");
@@ -2050,6 +2082,7 @@ int td3_train_step(td3_handle* h, rb_handle* rbh, int batch, void* stream, const
   } else {
     TD3_RC(run_body(h, actor_phase, inject_noise ? 1 : 0, s, r));
   }
+  TD3_RC(ring_end_read(r, s));                   // later adds wait for this step's reads
   if (inject_idx || inject_noise) TD3_HIP(hipStreamSynchronize(s));   // host sources are pageable
   return finish_step(h, actor_phase, s, stats);
 }
@@ -2123,7 +2156,7 @@ int td3_train_step_batch_particles(td3_handle* h, const float* feat, const float
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
   const int F = h->sd, ad = h->ad, B = P->B, Bp = P->Bp, np = h->N * h->D, c0 = kEncC2;
   const bool cdq = h->cdq != 0;
-  set_particle_source(P, P->pbatch, P->pbatch, 2 * np, 0, np, P->d_iota);
+  set_particle_source(P, kBatchSource, P->pbatch, 2 * np, 0, np, P->d_iota);
   if (inject_noise)
     TD3_HIP(hipMemcpyAsync(P->noise, inject_noise, (size_t)batch * ad * 4, hipMemcpyHostToDevice, s));
   // the sampled tensors -> MLP input rows and the packed particle rows (s | s')
@@ -2257,7 +2290,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   std::vector<hipEvent_t> ev(n + 1);
   for (auto& e : ev) TD3_HIP(hipEventCreate(&e));
   hipStream_t s = h->stream;
-  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
+  TD3_RC(ring_begin_read(r, s));
   TD3_HIP(hipEventRecord(ev[0], s));
   if (!fused) TD3_RC(input_from_ring(h, r, P, false, s));
   TD3_HIP(hipEventRecord(ev[1], s));
@@ -2265,6 +2298,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
     TD3_RC(st[i].run(s));
     TD3_HIP(hipEventRecord(ev[i + 2], s));
   }
+  TD3_RC(ring_end_read(r, s));
   TD3_HIP(hipStreamSynchronize(s));
   h->stage_names.clear();
   h->stage_kernels.clear();

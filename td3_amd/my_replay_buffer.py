@@ -238,6 +238,7 @@ class ReplayBuffer_featured(object):
 
     def load(self, folder):
         """my_replay_buffer.py:101-107 (pickles are read by an int-only unpickler)."""
+        self._pending = []                  # rows added before a load are replaced with it
         ptr = _load_int(os.path.join(folder, "ptr.pkl"))
         size = _load_int(os.path.join(folder, "size.pkl"))
         arrs = {}
@@ -441,6 +442,7 @@ class ReplayBuffer_particles(object):
 
     def load(self, folder):
         """my_replay_buffer.py:34-44 (int-only unpickler for ptr / size)."""
+        self._pending = []                  # rows added before a load are replaced with it
         ptr = _load_int(os.path.join(folder, "ptr.pkl"))
         size = _load_int(os.path.join(folder, "size.pkl"))
         arrs = {}

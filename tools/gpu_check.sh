@@ -3,7 +3,7 @@
 set -o pipefail
 tag=${1:-run}; shift
 mkdir -p gpurun_out
-timeout -k 10 300 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_$tag.log 2>&1
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$tag.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_$tag.log; echo "pytest rc=$rc"
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python3 bench.py "$@" > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err
