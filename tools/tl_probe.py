@@ -33,6 +33,8 @@ def main():
     lib.td3_tl_read.restype = C.c_int
     lib.td3_tl_read.argtypes = [C.c_void_p, C.c_int]
     lib.td3_tl_clear.restype = C.c_int
+    lib.td3_clk_read.restype = C.c_int
+    lib.td3_clk_read.argtypes = [C.c_void_p, C.c_int]
     sd, ad, B = 17, 6, 256
     pol = TD3(Box((sd,)), Box((ad,)), max_action=1.0, norm="layer", device=0, seed=17, use_graph=False)
     rb = RB(Box((sd,)), Box((ad,)), max_size=100_000, device=0, seed=3)
@@ -83,13 +85,19 @@ def main():
             base = t0.min()
             span = (t3.max() - base) * 0.01
             spread = (t0.max() - base) * 0.01
+            clk = np.zeros((8192, 2), dtype=np.uint64)
+            lib.td3_clk_read(clk.ctypes.data, 8192)
+            ck = clk[(buf[:, 3] != 0)].astype(np.int64)
+            dt_rt = (t2 - t1).astype(np.float64)
+            ok = dt_rt > 20
+            mhz = np.median((ck[ok, 1] - ck[ok, 0]) / dt_rt[ok] * 100.0) if ok.any() else float("nan")
             pro = np.median(t1 - t0) * 0.01
             mf = np.median(t2 - t1) * 0.01
             ep = np.median(t3 - t2) * 0.01
             print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f} {len(v):4d} {span:6.2f} {spread:6.2f} "
                   f"{pro:5.2f} {mf:5.2f} {ep:5.2f} {(t1 - base).max() * 0.01:7.2f} {(t3 - base).max() * 0.01:7.2f}")
             t5, t6, t7 = v[:, 5], v[:, 6], v[:, 7]
-            fine = f"   mark5 {np.median(t5 - t0) * 0.01:5.2f}"
+            fine = f"   clock(mfma phase) {mhz:6.0f} MHz   mark5 {np.median(t5 - t0) * 0.01:5.2f}"
             if t6.min() > 0:
                 fine += f" mark6 {np.median(t6 - t0) * 0.01:5.2f} mark7 {np.median(t7 - t0) * 0.01:5.2f}"
             print(fine)
