@@ -44,7 +44,13 @@ enum RowKind : int {
   kRowActorHeadBwd = 3,  // dQ1/da (Q1 LN1 bwd, W1 action cols), tanh bwd, actor head + LN3 bwd
   kRowCriticLossP = 4,   // TD3_particles: the same over A Q outputs, optional CDQ
   kRowActorLossP = 5,    // TD3_particles: -mean over B*A
-  kRowActorHeadBwdP = 6  // TD3_particles: dQ1/da through lnorm1, tanh bwd, actor head + LN3 bwd
+  kRowActorHeadBwdP = 6, // TD3_particles: dQ1/da through lnorm1, tanh bwd, actor head + LN3 bwd
+  // The twin critic's backward runs on UNIT loss gradients (dL/dQ_r = 1): every per-row
+  // gradient vector of the MLP backward is linear in the row's dL/dQ_r, so the dX chain does not
+  // wait for the clipped double-Q target; the dW stage scales row r by g_r = 2/B (Q_r - y_r).
+  kRowUnitLoss = 7,      // Q_j head, LN3 of Q_j, unit dU3 / dZ3 rows of Q_j
+  kRowTargetLoss = 8,    // target heads -> y (:140-142), g_j = 2/B (Q_j - y) (:148), squared errors
+  kRowLnBwd = 9,         // dZ = relu'(LN_bwd(dU)) of full rows (layer 0, no GEMM follows)
 };
 
 constexpr int kMaxEx = 24;
@@ -147,6 +153,8 @@ struct DwProb {
   int ntk;                        // k tiles of the weight
   int tile_begin;                 // matrix tiles: (Np/T)*ntk (T = 32, or 64 with tile64), then
                                   // vector tiles: Np/32
+  const float* rs; int ldrs;      // row scale of dZ / dU (unit-gradient backward): rs[r * ldrs];
+                                  // ldrs = 0 with rs -> 1.0f when the rows are the gradients
 };
 
 enum DwMode : int { kDwGrad = 0, kDwAdam = 1, kDwAdamPolyak = 2 };
@@ -165,12 +173,15 @@ struct DwArgs {
   AdamArgs adam;
   int mode;
   int tile64;                     // 1: dw64_kernel (64x64 tiles, ntk counts k tiles of 64)
+  int scaled;                     // 1: rows scaled by DwProb::rs (dw_kernel<true> / dw64_kernel<true>)
 };
 
 // ------------------------------------------------------------------ launchers (kernels.hip)
 int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds_bytes,
                 Counters* bump, int bump_actor, hipStream_t s);
 int launch_rows(int kind, const GemmTable& t, int Bp, hipStream_t s);
+// Two row kinds in one launch: problems [0, n1) run kind1, [n1, nprob) kind2.
+int launch_rows2(int kind1, int kind2, int n1, const GemmTable& t, int Bp, hipStream_t s);
 int launch_heads(const HeadArgs& a, int nprob, hipStream_t s);
 int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s);
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s);

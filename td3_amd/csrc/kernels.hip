@@ -856,13 +856,136 @@ __device__ __forceinline__ void row_actor_head_bwd_p(const GemmProb& P, const Ro
 #define TD3_ROW_WAVES 1
 #endif
 constexpr int kRowWaves = TD3_ROW_WAVES;   // waves (rows) per row-kernel workgroup: 1 (A/B 4 / 2 / 1: C2 8.93k / 9.03k / 9.09k; the waves of a row stage spread over 4x the CUs, whose load units they no longer share)
+// ---- unit-gradient critic head (kRowUnitLoss) ----------------------------------------------
+// The Q_j head (TD3_featured.py:145, Q.forward :74-81) and the backward of its mse term with
+// dL/dQ_j = 1: every per-row gradient vector of the MLP backward is linear in the row's
+// dL/dQ_j (LayerNorm backward and relu' are linear in the incoming gradient for fixed forward
+// activations), so the input-grad chain runs on these unit rows while the target path is still
+// computing y; the dW stage scales row r by g_r = 2/B (Q_j,r - y_r) (kRowTargetLoss).
+// ex[0]=H3_j ex[1]=gamma3 ex[2]=beta3 ex[3]=w4 ex[4]=b4
+// out: ex[5]=Q_j ex[6]=U3_j ex[7]=stats3_j ex[8]=dU3_j (unit: w4) Aout=dZ3_j (unit)
+// exi[0]=K3 exi[1]=ld3
+template <bool NORM>
+__device__ __forceinline__ void row_unit_loss(const GemmProb& P, const RowCtx& c) {
+  asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]),
+               "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.Aout), "s"(P.ldao));
+  const int K3 = P.exi[0], ld3 = P.exi[1];
+  float x[1][8], h[1][8], g[8], bb[8], w[8], mean[1] = {0.f}, rstd[1] = {1.f};
+  rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
+  if (NORM) {
+    rv_load(g, P.ex[1], ld3, c.lane);
+    rv_load(bb, P.ex[2], ld3, c.lane);
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) g[jj] = bb[jj] = 0.f;
+  }
+  rv_load(w, P.ex[3], ld3, c.lane);
+  const float b4 = gld(P.ex[4]);
+  __builtin_amdgcn_sched_barrier(0);     // every load requested before the first use
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) h[0][jj] = x[0][jj];
+  if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+  const float q = wsum(rv_pdot(x[0], w, K3, c.lane)) + b4;
+  if (c.lane == 0) {
+    gst(P.ex[5] + c.row, q);
+    if (NORM) {
+      gst(P.ex[7] + c.row, mean[0]);
+      gst(P.ex[7] + (c.Bp + c.row), rstd[0]);
+    }
+  }
+  if (NORM) rv_store(P.ex[6] + (size_t)c.row * ld3, ld3, c.lane, x[0]);
+  float gu[1][8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) gu[0][jj] = w[jj];
+  rv_store(P.ex[8] + (size_t)c.row * ld3, ld3, c.lane, gu[0]);
+  ln_bwd_rows<1>(gu, h, g, mean, rstd, K3, c.lane, NORM);
+  rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu[0]);
+}
+
+// ---- clipped double-Q target and the rows' loss gradients (kRowTargetLoss) -----------------
+// y = r + not_done * discount * min(Q1'(s',a'), Q2'(s',a')) (TD3_featured.py:140-142) and for both
+// online critics g_j = 2/B (Q_j - y) (F.mse_loss backward, :148): the head's dZ4_j and the row
+// scale of Q_j's unit backward in the dW stage; the squared errors for the loss read-back.
+// ex[0..1]=H3 of target q1 / q2  ex[2..3]=gamma3  ex[4..5]=beta3  ex[6..7]=w4  ex[8..9]=b4
+// ex[10]=reward ex[11]=not_done ex[12..13]=Q_1 / Q_2 (kRowUnitLoss)
+// out: ex[14]=y ex[15..16]=dZ4 of q1 / q2 (ld 32) ex[17]=sqerr [2][Bp] ex[18..19]=g of q1 / q2 [Bp]
+// exi[0]=K3 exi[1]=ld3   exf[0]=discount exf[1]=2/B
+template <bool NORM>
+__device__ __forceinline__ void row_target_loss(const GemmProb& P, const RowCtx& c) {
+  asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]),
+               "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.ex[11]),
+               "s"(P.ex[12]), "s"(P.ex[13]), "s"(P.exi[0]), "s"(P.exi[1]));
+  asm volatile("" ::"s"(P.ex[14]), "s"(P.ex[15]), "s"(P.ex[16]), "s"(P.ex[17]), "s"(P.ex[18]), "s"(P.ex[19]),
+               "s"(P.exf[0]), "s"(P.exf[1]), "s"(P.B));
+  const int K3 = P.exi[0], ld3 = P.exi[1];
+  float x0[1][8], x1[1][8], g[2][8], bb[2][8], w[2][8];
+  rv_load(x0[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
+  rv_load(x1[0], P.ex[1] + (size_t)c.row * ld3, ld3, c.lane);
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    if (NORM) {
+      rv_load(g[n], P.ex[2 + n], ld3, c.lane);
+      rv_load(bb[n], P.ex[4 + n], ld3, c.lane);
+    }
+    rv_load(w[n], P.ex[6 + n], ld3, c.lane);
+  }
+  const float b40 = gld(P.ex[8]), b41 = gld(P.ex[9]);
+  const float rw = gld(P.ex[10] + c.row), nd = gld(P.ex[11] + c.row);
+  const float q1 = gld(P.ex[12] + c.row), q2 = gld(P.ex[13] + c.row);
+  __builtin_amdgcn_sched_barrier(0);     // every load requested before the first use
+  float m0[1], s0[1], m1[1], s1[1];
+  if (NORM) {
+    ln_fwd_rows<1>(x0, g[0], bb[0], K3, c.lane, m0, s0);
+    ln_fwd_rows<1>(x1, g[1], bb[1], K3, c.lane, m1, s1);
+  }
+  const float d0 = rv_pdot(x0[0], w[0], K3, c.lane);
+  const float d1 = rv_pdot(x1[0], w[1], K3, c.lane);
+  const float tq0 = wsum(d0) + b40, tq1 = wsum(d1) + b41;
+  const float y = rw + (nd * P.exf[0]) * fminf(tq0, tq1);                  // :141-142
+  const bool live = c.row < P.B;
+  const float e1 = q1 - y, e2 = q2 - y;
+  const float g1 = live ? P.exf[1] * e1 : 0.f, g2 = live ? P.exf[1] * e2 : 0.f;   // mse_loss bwd (:148)
+  if (c.lane == 0) {
+    gst(P.ex[14] + c.row, y);
+    gst(P.ex[15] + ((size_t)c.row * 32), g1);
+    gst(P.ex[16] + ((size_t)c.row * 32), g2);
+    gst(P.ex[17] + c.row, live ? e1 * e1 : 0.f);
+    gst(P.ex[17] + (c.Bp + c.row), live ? e2 * e2 : 0.f);
+    gst(P.ex[18] + c.row, g1);
+    gst(P.ex[19] + c.row, g2);
+  }
+}
+
+// ---- dZ = relu'(LN_bwd(dU)) of full rows (kRowLnBwd): lnbwd_rows_kernel's row as a row kind,
+// so it can share a launch with another row stage.
+// ex[0]=dU ex[1]=H ex[2]=stats ex[3]=gamma  out: ex[4]=dZ   exi[0]=ld exi[1]=K
+template <bool NORM>
+__device__ __forceinline__ void row_lnbwd(const GemmProb& P, const RowCtx& c) {
+  asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.exi[0]),
+               "s"(P.exi[1]));
+  const int ld = P.exi[0];
+  float gu[1][8], h[1][8], g[8], mean[1], rstd[1];
+  float4 qg[2], qu[2], qh[2];
+  if constexpr (NORM) rv_load_raw(qg, P.ex[3], ld, c.lane);
+  rv_load_raw(qu, P.ex[0] + (size_t)c.row * ld, ld, c.lane);
+  rv_load_raw(qh, P.ex[1] + (size_t)c.row * ld, ld, c.lane);
+  mean[0] = NORM ? gld(P.ex[2] + c.row) : 0.f;
+  rstd[0] = NORM ? gld(P.ex[2] + (c.Bp + c.row)) : 1.f;
+  __builtin_amdgcn_sched_barrier(0);     // every load requested before the first use
+  if constexpr (NORM) rv_from_raw(g, qg, ld, c.lane);
+  else {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) g[jj] = 0.f;
+  }
+  rv_from_raw(gu[0], qu, ld, c.lane);
+  rv_from_raw(h[0], qh, ld, c.lane);
+  if constexpr (NORM) ln_bwd_rows_pk<1>(gu, h, g, mean, rstd, 1.0f / (float)P.exi[1]);
+  else ln_bwd_rows<1>(gu, h, g, mean, rstd, P.exi[1], c.lane, 0);
+  rv_store(P.ex[4] + (size_t)c.row * ld, ld, c.lane, gu[0]);
+}
+
 template <int KIND, bool NORM>
-__global__ __launch_bounds__(64 * kRowWaves) void row_kernel(int Bp, GemmTable tab) {   // Bp first: preloaded
-  const GemmProb& P = tab.p[blockIdx.y];
-  // grid.x = Bp / kRowWaves exactly (launch_rows): every wave owns a row, no bounds check (which would put
-  // a kernel-argument round trip ahead of the row's loads)
-  const RowCtx c{(int)(blockIdx.x * kRowWaves + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
-  TL_MARK(0);
+__device__ __forceinline__ void row_dispatch(const GemmProb& P, const RowCtx& c) {
   if constexpr (KIND == kRowPolicyHead) row_policy_head<NORM>(P, c);
   else if constexpr (KIND == kRowCriticLoss) row_critic_loss<NORM>(P, c);
   else if constexpr (KIND == kRowActorLoss) row_actor_loss<NORM>(P, c);
@@ -870,6 +993,31 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_kernel(int Bp, GemmTable t
   else if constexpr (KIND == kRowCriticLossP) row_critic_loss_p<NORM>(P, c);
   else if constexpr (KIND == kRowActorLossP) row_actor_loss_p<NORM>(P, c);
   else if constexpr (KIND == kRowActorHeadBwdP) row_actor_head_bwd_p<NORM>(P, c);
+  else if constexpr (KIND == kRowUnitLoss) row_unit_loss<NORM>(P, c);
+  else if constexpr (KIND == kRowTargetLoss) row_target_loss<NORM>(P, c);
+  else if constexpr (KIND == kRowLnBwd) row_lnbwd<NORM>(P, c);
+}
+
+template <int KIND, bool NORM>
+__global__ __launch_bounds__(64 * kRowWaves) void row_kernel(int Bp, GemmTable tab) {   // Bp first: preloaded
+  const GemmProb& P = tab.p[blockIdx.y];
+  // grid.x = Bp / kRowWaves exactly (launch_rows): every wave owns a row, no bounds check (which would put
+  // a kernel-argument round trip ahead of the row's loads)
+  const RowCtx c{(int)(blockIdx.x * kRowWaves + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
+  TL_MARK(0);
+  row_dispatch<KIND, NORM>(P, c);
+  TL_MARK(3);
+}
+
+// Two independent row stages in one launch (problems [0, n1) of kind K1, the rest K2): the
+// branch is on blockIdx.y, uniform per workgroup.
+template <int K1, int K2, bool NORM>
+__global__ __launch_bounds__(64 * kRowWaves) void row_kernel2(int Bp, int n1, GemmTable tab) {
+  const GemmProb& P = tab.p[blockIdx.y];
+  const RowCtx c{(int)(blockIdx.x * kRowWaves + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
+  TL_MARK(0);
+  if ((int)blockIdx.y < n1) row_dispatch<K1, NORM>(P, c);
+  else row_dispatch<K2, NORM>(P, c);
   TL_MARK(3);
 }
 
@@ -1395,8 +1543,11 @@ __device__ __forceinline__ void apply_grads(const DwArgs& a, const AdamK& k, con
   apply_grads_loaded<N>(a, k, idx, g, ok, st);
 }
 
+// The dZ rows' scale (unit-gradient rows: g_r; otherwise 1.0 from ldrs = 0) is requested with the
+// chunk, as 4 float4 (rows rb .. rb+15 of the dense scale array), so its wait is the chunk's own.
+template <bool SC>
 __device__ __forceinline__ void dw_load_chunk(const DwProb& P, int rc, int h, int n0, int k0, int i,
-                                              float (&av)[16], float (&bv)[16]) {
+                                              float (&av)[16], float (&bv)[16], float4 (&sc)[4]) {
   const int rb = rc * 32 + 16 * h;
   const float* gp = P.G + (size_t)rb * P.ldg + n0 + i;
   const float* up = P.U + (size_t)rb * P.ldu + k0 + i;
@@ -1405,11 +1556,23 @@ __device__ __forceinline__ void dw_load_chunk(const DwProb& P, int rc, int h, in
     av[s] = gld(gp + (size_t)s * P.ldg);
     bv[s] = gld(up + (size_t)s * P.ldu);
   }
+  if constexpr (SC) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sc[q] = gld4(P.rs + (size_t)(rb + 4 * q) * P.ldrs);
+  }
+}
+template <bool SC>
+__device__ __forceinline__ void dw_scale(float (&av)[16], const float4 (&sc)[4]) {
+  if constexpr (!SC) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    av[4 * q + 0] *= sc[q].x; av[4 * q + 1] *= sc[q].y; av[4 * q + 2] *= sc[q].z; av[4 * q + 3] *= sc[q].w;
+  }
 }
 
 // dw64_kernel's vector tile (Bp >= 512): one column per thread, NT/32 row groups of 8-row strides
 // (the float4 form below measured slower there: Humanoid C_dw 52 -> 61 us).
-template <int NT>
+template <int NT, bool SC>
 __device__ __forceinline__ void dw_vector_tile_cols(const DwArgs& a, const DwProb& P, const AdamK& k, int j,
                                                float* red) {
   constexpr int NG = NT / 32;
@@ -1423,9 +1586,10 @@ __device__ __forceinline__ void dw_vector_tile_cols(const DwArgs& a, const DwPro
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int r = min(r0 + NG * u, a.Bp - 1);     // clamped: loads stay unconditional
-      gz[u] = hasb ? gld(P.G + ((size_t)r * P.ldg + n0 + c)) : 0.f;
+      const float sc = SC ? gld(P.rs + (size_t)r * P.ldrs) : 1.f;   // dZ / dU row scale (unit rows)
+      gz[u] = hasb ? gld(P.G + ((size_t)r * P.ldg + n0 + c)) * sc : 0.f;
       if (ln) {
-        gu[u] = gld(P.GU + ((size_t)r * P.ldgu + n0 + c));
+        gu[u] = gld(P.GU + ((size_t)r * P.ldgu + n0 + c)) * sc;
         hh[u] = gld(P.H + ((size_t)r * P.ldh + n0 + c));
         mu[u] = gld(P.stats + r);
         rs[u] = gld(P.stats + (a.Bp + r));
@@ -1467,7 +1631,7 @@ __device__ __forceinline__ void dw_vector_tile_cols(const DwArgs& a, const DwPro
 // then the optimizer update of those 32 columns.  A thread owns 4 adjacent columns (float4 loads)
 // of every (NT/8)-th row: at Bp = 256 all of a thread's rows are requested in one batch, and the
 // optimizer state of the 32 x 3 elements is requested behind them.
-template <int NT>
+template <int NT, bool SC>
 __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P, const AdamPw& pw, int j,
                                                float* red) {
   constexpr int RG = NT / 8;                        // row groups
@@ -1491,7 +1655,7 @@ __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P,
   const int ldz = hasb ? P.ldg : P.ldgu, ldu = ln ? P.ldgu : P.ldg, ldh = ln ? P.ldh : P.ldg;
   for (int r0 = rg; r0 < a.Bp; r0 += RG * U) {
     float4 gz[U], gu[U], hh[U];
-    float mu[U], rs[U];
+    float mu[U], rs[U], sc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = min(r0 + RG * u, a.Bp - 1);     // clamped: loads stay unconditional
@@ -1500,6 +1664,7 @@ __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P,
       hh[u] = gld4(hp + ((size_t)r * ldh + n0 + c4));
       mu[u] = gld(stp + r);
       rs[u] = gld(stp + (a.Bp + r));
+      sc[u] = SC ? gld(P.rs + (size_t)r * P.ldrs) : 1.f;   // dZ / dU row scale (unit rows)
     }
     if (r0 == rg && threadIdx.x < 32) adam_state_load<3>(a, idx, ok, st);
     __builtin_amdgcn_sched_barrier(0);
@@ -1510,10 +1675,10 @@ __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P,
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (r0 + RG * u >= a.Bp) continue;
-      const float z[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
+      const float z[4] = {gz[u].x * sc[u], gz[u].y * sc[u], gz[u].z * sc[u], gz[u].w * sc[u]};
       sb[0] += z[0]; sb[1] += z[1]; sb[2] += z[2]; sb[3] += z[3];
       if (ln) {
-        const float g4[4] = {gu[u].x, gu[u].y, gu[u].z, gu[u].w};
+        const float g4[4] = {gu[u].x * sc[u], gu[u].y * sc[u], gu[u].z * sc[u], gu[u].w * sc[u]};
         const float h4[4] = {hh[u].x, hh[u].y, hh[u].z, hh[u].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1553,6 +1718,8 @@ __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P,
 #ifndef TD3_DW_OCC
 #define TD3_DW_OCC 3
 #endif
+// SC: the launch scales dZ / dU rows (DwProb::rs; the unit-gradient critic backward)
+template <bool SC>
 __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
   __shared__ float red[4 * 32 * 33];
   const int b = xcd_tile(nb);
@@ -1577,8 +1744,9 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     float a0[16], b0[16], a1[16], b1[16];
-    if (cb < ce) dw_load_chunk(P, cb, h, n0, k0, i, a0, b0);
-    if (cb + 1 < ce) dw_load_chunk(P, cb + 1, h, n0, k0, i, a1, b1);
+    float4 c0[4], c1[4];
+    if (cb < ce) dw_load_chunk<SC>(P, cb, h, n0, k0, i, a0, b0, c0);
+    if (cb + 1 < ce) dw_load_chunk<SC>(P, cb + 1, h, n0, k0, i, a1, b1, c1);
     // the optimizer state of this thread's 4 elements (row tn, columns tq..tq+3 of the tile: one
     // float4 per array, a quarter of the memory instructions of 4 scalar elements), requested
     // behind the first two operand chunks (their MFMA waits do not include it) and landing during
@@ -1595,13 +1763,15 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
       st4 = gld4((pol ? a.adam.T : a.adam.P) + ix);
     }
     for (int rc = cb; rc < ce; rc += 2) {
+      dw_scale<SC>(a0, c0);
 #pragma unroll
       for (int s = 0; s < 16; ++s) acc = mfma32x32x2(a0[s], b0[s], acc);
-      if (rc + 2 < ce) dw_load_chunk(P, rc + 2, h, n0, k0, i, a0, b0);
+      if (rc + 2 < ce) dw_load_chunk<SC>(P, rc + 2, h, n0, k0, i, a0, b0, c0);
       if (rc + 1 >= ce) break;
+      dw_scale<SC>(a1, c1);
 #pragma unroll
       for (int s = 0; s < 16; ++s) acc = mfma32x32x2(a1[s], b1[s], acc);
-      if (rc + 3 < ce) dw_load_chunk(P, rc + 3, h, n0, k0, i, a1, b1);
+      if (rc + 3 < ce) dw_load_chunk<SC>(P, rc + 3, h, n0, k0, i, a1, b1, c1);
     }
     TL_MARK(5);
 #pragma unroll
@@ -1640,7 +1810,7 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
     TL_MARK(3);
     return;
   }
-  dw_vector_tile<256>(a, P, pw, t - nmat, red);
+  dw_vector_tile<256, SC>(a, P, pw, t - nmat, red);
 }
 
 // Large batches (Bp >= 512): 64x64 weight tiles per workgroup of 8 waves.  Each step stages 64
@@ -1650,6 +1820,7 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
 // at B >= 512.  The two row halves meet in LDS; the rh=0 waves apply the optimizer update.
 constexpr int kDw64S = 66;                          // LDS row stride: rows 16 apart 32 banks apart
 constexpr int kDw64Depth = 2;                       // 64-row steps in flight (1, 3, 5: no change)
+template <bool SC>
 __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   __shared__ float sm[2 * 2 * 64 * kDw64S];         // [buf][operand][64 rows][kDw64S]
   const int b = xcd_tile(nb);
@@ -1664,7 +1835,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   const int nmat = ntn * P.ntk;                      // ntk = k tiles of 64 in this mode
   const AdamPw pw = adam_pw(a.adam);
   if (t >= nmat) {
-    dw_vector_tile_cols<512>(a, P, make_adam(a.adam, pw), t - nmat, sm);
+    dw_vector_tile_cols<512, SC>(a, P, make_adam(a.adam, pw), t - nmat, sm);
     return;
   }
   const int kt = t % P.ntk, nt = t / P.ntk;
@@ -1675,16 +1846,18 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   // kDw64Depth steps of 64 rows are in flight in registers (HBM latency > one step's 16 MFMAs)
   constexpr int D = kDw64Depth;
   float4 sg[D][2], su[D][2];
-  auto fetch = [&](int r0, float4 (&g)[2], float4 (&u)[2]) {
+  float ssc[D][2];
+  auto fetch = [&](int r0, float4 (&g)[2], float4 (&u)[2], float (&sc)[2]) {
 #pragma unroll
     for (int v = 0; v < 2; ++v) {
       const int e = tid + 512 * v, row = r0 + (e >> 4), c4 = (e & 15) * 4;
       const bool live = row < a.Bp;
       g[v] = (live && n0 + c4 < P.Np) ? gld4(P.G + (size_t)row * P.ldg + n0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
       u[v] = (live && k0 + c4 < P.Kp) ? gld4(P.U + (size_t)row * P.ldu + k0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      sc[v] = SC ? gld(P.rs + (size_t)min(row, a.Bp - 1) * P.ldrs) : 1.f;   // dZ row scale (unit rows)
     }
   };
-  auto put = [&](int buf, const float4 (&gq)[2], const float4 (&uq)[2]) {
+  auto put = [&](int buf, const float4 (&gq)[2], const float4 (&uq)[2], const float (&sc)[2]) {
     float* g = sm + buf * 2 * 64 * kDw64S;
     float* uu = g + 64 * kDw64S;
 #pragma unroll
@@ -1692,7 +1865,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
       const int e = tid + 512 * v, row = e >> 4, c4 = (e & 15) * 4;
       float* gp = g + row * kDw64S + c4;
       float* up = uu + row * kDw64S + c4;
-      gp[0] = gq[v].x; gp[1] = gq[v].y; gp[2] = gq[v].z; gp[3] = gq[v].w;
+      gp[0] = gq[v].x * sc[v]; gp[1] = gq[v].y * sc[v]; gp[2] = gq[v].z * sc[v]; gp[3] = gq[v].w * sc[v];
       up[0] = uq[v].x; up[1] = uq[v].y; up[2] = uq[v].z; up[3] = uq[v].w;
     }
   };
@@ -1702,16 +1875,16 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   const int nstep = (a.Bp + 63) >> 6;
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    if (d < nstep) fetch(d * 64, sg[d], su[d]);
+    if (d < nstep) fetch(d * 64, sg[d], su[d], ssc[d]);
   for (int st0 = 0; st0 < nstep; st0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const int st = st0 + d;
       if (st >= nstep) break;
       const int buf = st & 1;
-      put(buf, sg[d], su[d]);
+      put(buf, sg[d], su[d], ssc[d]);
       __syncthreads();
-      if (st + D < nstep) fetch((st + D) * 64, sg[d], su[d]);
+      if (st + D < nstep) fetch((st + D) * 64, sg[d], su[d], ssc[d]);
       const float* g = sm + buf * 2 * 64 * kDw64S + (rh * 32 + 16 * h) * kDw64S;
       const float* uu = g + 64 * kDw64S;
 #pragma unroll
@@ -1853,6 +2026,32 @@ int launch_rows(int kind, const GemmTable& d, int Bp, hipStream_t s) {
   return 0;
 }
 
+template <bool NORM>
+static int launch_rows2_t(int k1, int k2, int n1, const GemmTable& d, int Bp, hipStream_t s) {
+  const dim3 grid(Bp / kRowWaves, d.nprob);
+  if (k1 == kRowPolicyHead && k2 == kRowUnitLoss)
+    hipLaunchKernelGGL((row_kernel2<kRowPolicyHead, kRowUnitLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, n1, d);
+  else if (k1 == kRowTargetLoss && k2 == kRowLnBwd)
+    hipLaunchKernelGGL((row_kernel2<kRowTargetLoss, kRowLnBwd, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, n1, d);
+  else {
+    set_error("internal: row kinds %d + %d are not instantiated together", k1, k2);
+    return -1;
+  }
+  return 0;
+}
+
+int launch_rows2(int kind1, int kind2, int n1, const GemmTable& d, int Bp, hipStream_t s) {
+  if (n1 < 1 || n1 >= d.nprob) {
+    set_error("internal: launch_rows2 split %d of %d problems", n1, d.nprob);
+    return -1;
+  }
+  const int rc = d.p[0].norm ? launch_rows2_t<true>(kind1, kind2, n1, d, Bp, s)
+                             : launch_rows2_t<false>(kind1, kind2, n1, d, Bp, s);
+  if (rc) return rc;
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_heads(const HeadArgs& a, int nprob, hipStream_t s) {
   hipLaunchKernelGGL(head_kernel, dim3(a.Bp / 4, nprob), dim3(256), 0, s, a);
   TD3_HIP(hipGetLastError());
@@ -1872,10 +2071,14 @@ int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStr
 
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s) {
   if (nblocks <= 0) return 0;
-  if (a.tile64)
-    hipLaunchKernelGGL(dw64_kernel, dim3((nblocks + 7) & ~7), dim3(512), 0, s, a, nblocks);
-  else
-    hipLaunchKernelGGL(dw_kernel, dim3((nblocks + 7) & ~7), dim3(256), 0, s, a, nblocks);
+  const dim3 grid((nblocks + 7) & ~7);
+  if (a.tile64) {
+    if (a.scaled) hipLaunchKernelGGL(dw64_kernel<true>, grid, dim3(512), 0, s, a, nblocks);
+    else hipLaunchKernelGGL(dw64_kernel<false>, grid, dim3(512), 0, s, a, nblocks);
+  } else {
+    if (a.scaled) hipLaunchKernelGGL(dw_kernel<true>, grid, dim3(256), 0, s, a, nblocks);
+    else hipLaunchKernelGGL(dw_kernel<false>, grid, dim3(256), 0, s, a, nblocks);
+  }
   TD3_HIP(hipGetLastError());
   return 0;
 }

@@ -169,6 +169,7 @@ struct Plan {
   float *X_S = nullptr, *X_SA = nullptr, *X_S2 = nullptr, *X_S2A = nullptr, *X_SP = nullptr;
   int ld_s = 0, ld_sa = 0;
   float *R = nullptr, *ND = nullptr, *noise = nullptr, *Y = nullptr, *sqerr = nullptr;
+  float* gscale[2] = {};                // [Bp] g_r = 2/B (Q_j,r - y_r): row scale of Q_j's unit backward
   int64_t* d_idx = nullptr;
   int64_t* d_inject_idx = nullptr;
   EvalB TA, Q[2], A, TQ[2], AQ;
@@ -224,6 +225,7 @@ struct td3_handle {
   Group actor, critic;
   float* arena = nullptr;
   Counters* d_ctr = nullptr;
+  float* ones = nullptr;      // 64 x 1.0f: the row scale of dW problems whose rows are the gradients
   int64_t total_it = 0, critic_step = 0, actor_step = 0;   // host mirror
   // Adam hyper-parameters per optimizer, [0] critic, [1] actor (AdamArgs::which).  Both start
   // from the config; torch's Adam.load_state_dict adopts a checkpoint's param_groups, and so
@@ -346,6 +348,20 @@ static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<
   char kname[64];
   snprintf(kname, sizeof(kname), "td3::row_kernel<%d>", kind);
   st.push_back({name, [=](hipStream_t s) { return launch_rows(kind, t, Bp, s); }, 0, kname});
+  return 0;
+}
+
+// Two independent row stages in one launch: problems [0, n1) of kind1, the rest of kind2.
+static int push_row2_stage(std::vector<Stage>& st, std::vector<GemmProb>& probs, int kind1, int kind2, int n1,
+                           int Bp, const std::string& name) {
+  TD3_ARG(!probs.empty() && probs.size() <= (size_t)kMaxProbs, "too many problems in one row stage");
+  TD3_ARG(n1 >= 1 && n1 < (int)probs.size(), "internal: row stage split");
+  GemmTable t{};
+  for (size_t i = 0; i < probs.size(); ++i) t.p[i] = probs[i];
+  t.nprob = (int)probs.size();
+  char kname[64];
+  snprintf(kname, sizeof(kname), "td3::row_kernel2<%d, %d>", kind1, kind2);
+  st.push_back({name, [=](hipStream_t s) { return launch_rows2(kind1, kind2, n1, t, Bp, s); }, 0, kname});
   return 0;
 }
 
@@ -506,7 +522,8 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 // the input grad that feeds lnorm1's backward, the encoder and dQ1/da; replaces the dZ_0 rows.
 static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<BwdItem>& items, int Bp, int B, const char* tag,
-                          bool need_dz0, bool need_in = false) {
+                          bool need_dz0, bool need_in = false,
+                          std::vector<GemmProb>* lnbwd_rows = nullptr) {
   const bool norm = h->cfg.norm != 0;
   for (int l = 2; l >= (need_in ? 0 : 1); --l) {
     std::vector<GemmProb> probs;
@@ -558,6 +575,23 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, l == 2 ? kProCopy : kProLNBwd, Bp, lds, blocks,
                            flops, std::string(tag) + "_bwd" + std::to_string(l), nullptr, 0));
   }
+  if (need_dz0 && !need_in && lnbwd_rows) {     // as row problems for a shared row launch (kRowLnBwd)
+    for (auto& it : items) {
+      const LinearL& L = it.net->lin[0];
+      GemmProb p{};
+      p.norm = norm ? 1 : 0;
+      p.B = B;
+      p.ex[0] = it.e->GU[0];
+      p.ex[1] = it.e->H[0];
+      p.ex[2] = it.e->stats[0];
+      p.ex[3] = const_cast<float*>(it.P + it.net->ln[0].offg);
+      p.ex[4] = it.e->GZ[0];
+      p.exi[0] = L.Np;
+      p.exi[1] = L.N;
+      lnbwd_rows->push_back(p);
+    }
+    return 0;
+  }
   if (need_dz0 && !need_in) {
     LnBwdTable tab{};
     int np = 0;
@@ -587,9 +621,12 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 
 // Weight / bias / LN grads of every layer of `items`, fused with the optimizer.
 // enc (TD3_particles): the encoder partial slabs of `items` (reduced + optimizer in one launch).
+// unit_scale (featured critic): per item, the dense [Bp] row scale g_r of its unit-gradient
+// backward rows (layers 0..2 and their LayerNorms; the head's dZ is the true gradient already).
 static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                         Group& g, int which, const std::vector<BwdItem>& items, int Bp,
-                        const char* tag, bool polyak, int enc_nwg = 0) {
+                        const char* tag, bool polyak, int enc_nwg = 0,
+                        const std::vector<const float*>* unit_scale = nullptr) {
   const bool norm = h->cfg.norm != 0;
   // B >= 512: 64x64 weight tiles with LDS-staged operands (dw64_kernel: half the operand
   // traffic, Humanoid C_dw 73 -> 63 us), else 32x32 register tiles (dw_kernel: more, shorter
@@ -598,11 +635,16 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   std::vector<DwProb> probs;
   int blocks = 0;
   double flops = 0;
-  for (auto& it : items) {
+  TD3_ARG(!unit_scale || unit_scale->size() == items.size(), "internal: one row scale per dW item");
+  for (size_t k = 0; k < items.size(); ++k) {
+    const BwdItem& it = items[k];
     const NetL& n = *it.net;
+    const float* usc = unit_scale ? (*unit_scale)[k] : nullptr;
     for (int l = 0; l < 4; ++l) {
       const LinearL& L = n.lin[l];
       DwProb p{};
+      p.rs = (usc && l < 3) ? usc : h->ones;
+      p.ldrs = (usc && l < 3) ? 1 : 0;
       p.G = it.e->GZ[l];
       p.ldg = (l == 3) ? 32 : L.Np;
       p.U = (l == 0) ? (n.D > 0 ? it.e->Uin : it.e->X) : it.e->U[l - 1];
@@ -631,6 +673,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     }
     if (n.lnin) {                                   // lnorm1 affine grads (vector tiles only)
       DwProb p{};
+      p.rs = usc ? usc : h->ones;
+      p.ldrs = usc ? 1 : 0;
       p.Np = n.ln_in.Np;
       p.offb = -1;
       p.offg = n.ln_in.offg;
@@ -667,8 +711,9 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   const bool dp = h->comm != nullptr;
   a.mode = dp ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
   a.tile64 = tile64 ? 1 : 0;
+  a.scaled = unit_scale ? 1 : 0;
   st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
-                tile64 ? "td3::dw64_kernel" : "td3::dw_kernel"});
+                std::string(tile64 ? "td3::dw64_kernel<" : "td3::dw_kernel<") + (unit_scale ? "true>" : "false>")});
   if (enc_nwg > 0) {
     EncAdamArgs ea{};
     for (auto& it : items) {
@@ -740,6 +785,13 @@ static size_t eval_floats(const NetL& n, int Bp, bool bwd, bool norm) {
   return f;
 }
 
+// Critic phase on unit loss gradients (kRowUnitLoss / kRowTargetLoss, row-scaled dW): off keeps
+// the sequential order (heads -> target twin -> critic_loss -> input grads -> dW).
+#ifndef TD3_UNIT_CRITIC
+#define TD3_UNIT_CRITIC 1
+#endif
+constexpr bool kUnitCritic = TD3_UNIT_CRITIC != 0;
+
 static int build_step(td3_handle* h, int B) {
   std::unique_ptr<Plan> P(new Plan());
   const int Bp = pad32(B);
@@ -753,7 +805,7 @@ static int build_step(td3_handle* h, int B) {
   const NetL& an = h->actor.nets[0];
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[1];
-  size_t floats = (size_t)Bp * (2 * P->ld_s + 3 * P->ld_sa) + 8 * (size_t)Bp + (size_t)Bp * ad + 4096;
+  size_t floats = (size_t)Bp * (2 * P->ld_s + 3 * P->ld_sa) + 10 * (size_t)Bp + (size_t)Bp * ad + 4096;
   floats += eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, true, norm) +
             eval_floats(an, Bp, true, norm) + 2 * eval_floats(q1, Bp, false, norm) +
             eval_floats(q1, Bp, true, norm) + 1024;
@@ -774,6 +826,8 @@ static int build_step(td3_handle* h, int B) {
   P->sqerr = S.take(2 * (size_t)Bp);
   P->d_idx = (int64_t*)S.take(2 * (size_t)Bp);
   P->d_inject_idx = (int64_t*)S.take(2 * (size_t)Bp);
+  P->gscale[0] = S.take(Bp);
+  P->gscale[1] = S.take(Bp);
   alloc_eval(S, an, Bp, P->X_S2, P->ld_s, false, norm, false, P->TA);
   alloc_eval(S, q1, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[0]);
   alloc_eval(S, q2, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[1]);
@@ -855,61 +909,132 @@ static int build_step(td3_handle* h, int B) {
                               2 * sd + ad, true));
         P->body_ring[actor_phase][inj].push_back(fr[0]);
       }
-      // ---- heads: a' = target smoothing into X_S2A (:131-137); pi(s) into X_SP (:159)
-      {
-        std::vector<GemmProb> hp = {policy_head(Pta, P->TA, P->X_S2A, 1, inj ? 0 : 1)};
-        if (actor_phase) hp.push_back(policy_head(Pa, P->A, P->X_SP, 0, 0));
-        TD3_RC(push_row_stage(h, P->tables, st, hp, kRowPolicyHead, Bp, "heads"));
-      }
-      // ---- target twin on (s', a')
-      std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
-      TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, nullptr, nullptr, 0, true));
-      // ---- critic loss (clipped double-Q target, mse) and LN3 backward of the twin
-      {
-        std::vector<GemmProb> cl;
-        for (int j = 0; j < 2; ++j) {
-          const NetL& qj = j ? q2 : q1;
+      if (kUnitCritic) {
+        // Critic phase on unit loss gradients (kRowUnitLoss): the twin's input-grad chain runs
+        // between the heads and the target twin, independent of y; the target-loss row stage
+        // (y, g_j = 2/B (Q_j - y)) shares its launch with the layer-0 LN backward rows, and the
+        // dW stage scales the unit rows by g_j.  One launch fewer than the sequential order.
+        {
+          std::vector<GemmProb> hp = {policy_head(Pta, P->TA, P->X_S2A, 1, inj ? 0 : 1)};
+          if (actor_phase) hp.push_back(policy_head(Pa, P->A, P->X_SP, 0, 0));
+          const int n1 = (int)hp.size();
+          for (int j = 0; j < 2; ++j) {
+            const NetL& qj = j ? q2 : q1;
+            GemmProb p{};
+            p.norm = norm ? 1 : 0;
+            p.B = B;
+            p.ex[0] = P->Q[j].H[2];
+            p.ex[1] = const_cast<float*>(Pq1 + qj.ln[2].offg);
+            p.ex[2] = const_cast<float*>(Pq1 + qj.ln[2].offb);
+            p.ex[3] = const_cast<float*>(Pq1 + qj.lin[3].offW);
+            p.ex[4] = const_cast<float*>(Pq1 + qj.lin[3].offb);
+            p.ex[5] = P->Q[j].Qv;
+            p.ex[6] = P->Q[j].U[2];
+            p.ex[7] = P->Q[j].stats[2];
+            p.ex[8] = P->Q[j].GU[2];
+            p.Aout = P->Q[j].GZ[2];
+            p.ldao = qj.lin[2].Np;
+            p.exi[0] = qj.lin[2].N;
+            p.exi[1] = qj.lin[2].Np;
+            hp.push_back(p);
+          }
+          TD3_RC(push_row2_stage(st, hp, kRowPolicyHead, kRowUnitLoss, n1, Bp, "heads"));
+        }
+        std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0], true}, {&q2, Pq2, &P->Q[1], true}};
+        std::vector<GemmProb> rows;
+        {   // the target loss row problem first (kRowTargetLoss), the LN0 backward rows after it
           GemmProb p{};
           p.norm = norm ? 1 : 0;
           p.B = B;
           p.ex[0] = P->TQ[0].H[2];
           p.ex[1] = P->TQ[1].H[2];
-          p.ex[2] = P->Q[j].H[2];
-          p.ex[3] = const_cast<float*>(Ptq1 + q1.ln[2].offg);
-          p.ex[4] = const_cast<float*>(Ptq2 + q2.ln[2].offg);
-          p.ex[5] = const_cast<float*>(Pq1 + qj.ln[2].offg);
-          p.ex[6] = const_cast<float*>(Ptq1 + q1.ln[2].offb);
-          p.ex[7] = const_cast<float*>(Ptq2 + q2.ln[2].offb);
-          p.ex[8] = const_cast<float*>(Pq1 + qj.ln[2].offb);
-          p.ex[9] = const_cast<float*>(Ptq1 + q1.lin[3].offW);
-          p.ex[10] = const_cast<float*>(Ptq2 + q2.lin[3].offW);
-          p.ex[11] = const_cast<float*>(Pq1 + qj.lin[3].offW);
-          p.ex[12] = const_cast<float*>(Ptq1 + q1.lin[3].offb);
-          p.ex[13] = const_cast<float*>(Ptq2 + q2.lin[3].offb);
-          p.ex[14] = const_cast<float*>(Pq1 + qj.lin[3].offb);
-          p.ex[15] = P->R;
-          p.ex[16] = P->ND;
-          p.ex[17] = P->Q[j].GZ[3];
-          p.ex[18] = P->Q[j].GU[2];
-          p.ex[19] = P->Q[j].U[2];
-          p.ex[20] = P->Q[j].stats[2];
-          p.ex[21] = P->Y;
-          p.ex[22] = P->sqerr + (size_t)j * Bp;
-          p.ex[23] = P->Q[j].Qv;
-          p.Aout = P->Q[j].GZ[2];
-          p.ldao = qj.lin[2].Np;
-          p.exi[0] = qj.lin[2].N;
-          p.exi[1] = qj.lin[2].Np;
-          p.exi[2] = j;
+          p.ex[2] = const_cast<float*>(Ptq1 + q1.ln[2].offg);
+          p.ex[3] = const_cast<float*>(Ptq2 + q2.ln[2].offg);
+          p.ex[4] = const_cast<float*>(Ptq1 + q1.ln[2].offb);
+          p.ex[5] = const_cast<float*>(Ptq2 + q2.ln[2].offb);
+          p.ex[6] = const_cast<float*>(Ptq1 + q1.lin[3].offW);
+          p.ex[7] = const_cast<float*>(Ptq2 + q2.lin[3].offW);
+          p.ex[8] = const_cast<float*>(Ptq1 + q1.lin[3].offb);
+          p.ex[9] = const_cast<float*>(Ptq2 + q2.lin[3].offb);
+          p.ex[10] = P->R;
+          p.ex[11] = P->ND;
+          p.ex[12] = P->Q[0].Qv;
+          p.ex[13] = P->Q[1].Qv;
+          p.ex[14] = P->Y;
+          p.ex[15] = P->Q[0].GZ[3];
+          p.ex[16] = P->Q[1].GZ[3];
+          p.ex[17] = P->sqerr;
+          p.ex[18] = P->gscale[0];
+          p.ex[19] = P->gscale[1];
+          p.exi[0] = q1.lin[2].N;
+          p.exi[1] = q1.lin[2].Np;
           p.exf[0] = (float)h->cfg.discount;
           p.exf[1] = (float)(2.0 / (double)B);
-          cl.push_back(p);
+          rows.push_back(p);
         }
-        TD3_RC(push_row_stage(h, P->tables, st, cl, kRowCriticLoss, Bp, "critic_loss"));
+        TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true, false, &rows));
+        std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
+        TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, nullptr, nullptr, 0, true));
+        TD3_RC(push_row2_stage(st, rows, kRowTargetLoss, kRowLnBwd, 1, Bp, "critic_loss"));
+        const std::vector<const float*> usc = {P->gscale[0], P->gscale[1]};
+        TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, 0, &usc));
+      } else {
+        // ---- heads: a' = target smoothing into X_S2A (:131-137); pi(s) into X_SP (:159)
+        {
+          std::vector<GemmProb> hp = {policy_head(Pta, P->TA, P->X_S2A, 1, inj ? 0 : 1)};
+          if (actor_phase) hp.push_back(policy_head(Pa, P->A, P->X_SP, 0, 0));
+          TD3_RC(push_row_stage(h, P->tables, st, hp, kRowPolicyHead, Bp, "heads"));
+        }
+        // ---- target twin on (s', a')
+        std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
+        TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, nullptr, nullptr, 0, true));
+        // ---- critic loss (clipped double-Q target, mse) and LN3 backward of the twin
+        {
+          std::vector<GemmProb> cl;
+          for (int j = 0; j < 2; ++j) {
+            const NetL& qj = j ? q2 : q1;
+            GemmProb p{};
+            p.norm = norm ? 1 : 0;
+            p.B = B;
+            p.ex[0] = P->TQ[0].H[2];
+            p.ex[1] = P->TQ[1].H[2];
+            p.ex[2] = P->Q[j].H[2];
+            p.ex[3] = const_cast<float*>(Ptq1 + q1.ln[2].offg);
+            p.ex[4] = const_cast<float*>(Ptq2 + q2.ln[2].offg);
+            p.ex[5] = const_cast<float*>(Pq1 + qj.ln[2].offg);
+            p.ex[6] = const_cast<float*>(Ptq1 + q1.ln[2].offb);
+            p.ex[7] = const_cast<float*>(Ptq2 + q2.ln[2].offb);
+            p.ex[8] = const_cast<float*>(Pq1 + qj.ln[2].offb);
+            p.ex[9] = const_cast<float*>(Ptq1 + q1.lin[3].offW);
+            p.ex[10] = const_cast<float*>(Ptq2 + q2.lin[3].offW);
+            p.ex[11] = const_cast<float*>(Pq1 + qj.lin[3].offW);
+            p.ex[12] = const_cast<float*>(Ptq1 + q1.lin[3].offb);
+            p.ex[13] = const_cast<float*>(Ptq2 + q2.lin[3].offb);
+            p.ex[14] = const_cast<float*>(Pq1 + qj.lin[3].offb);
+            p.ex[15] = P->R;
+            p.ex[16] = P->ND;
+            p.ex[17] = P->Q[j].GZ[3];
+            p.ex[18] = P->Q[j].GU[2];
+            p.ex[19] = P->Q[j].U[2];
+            p.ex[20] = P->Q[j].stats[2];
+            p.ex[21] = P->Y;
+            p.ex[22] = P->sqerr + (size_t)j * Bp;
+            p.ex[23] = P->Q[j].Qv;
+            p.Aout = P->Q[j].GZ[2];
+            p.ldao = qj.lin[2].Np;
+            p.exi[0] = qj.lin[2].N;
+            p.exi[1] = qj.lin[2].Np;
+            p.exi[2] = j;
+            p.exf[0] = (float)h->cfg.discount;
+            p.exf[1] = (float)(2.0 / (double)B);
+            cl.push_back(p);
+          }
+          TD3_RC(push_row_stage(h, P->tables, st, cl, kRowCriticLoss, Bp, "critic_loss"));
+        }
+        std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0], true}, {&q2, Pq2, &P->Q[1], true}};
+        TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true));
+        TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0));
       }
-      std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0], true}, {&q2, Pq2, &P->Q[1], true}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true));
-      TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0));
       if (!actor_phase) continue;
       // ---------------- delayed policy update (TD3_featured.py:156-171)
       std::vector<FwdItem> f3 = {{&q1, Pq1, &P->AQ, false, true}};
@@ -1883,6 +2008,12 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   }
   TD3_HIP(hipMalloc(&h->d_ctr, sizeof(Counters)));
   {
+    float one[64];
+    for (float& v : one) v = 1.0f;
+    TD3_HIP(hipMalloc(&h->ones, sizeof(one)));
+    TD3_HIP(hipMemcpy(h->ones, one, sizeof(one), hipMemcpyHostToDevice));
+  }
+  {
     const Counters c0 = make_counters(h, 0, 0, 0);
     TD3_HIP(hipMemcpy(h->d_ctr, &c0, sizeof(c0), hipMemcpyHostToDevice));
   }
@@ -1906,6 +2037,7 @@ int td3_destroy(td3_handle* h) {
   if (h->comm) ncclCommDestroy(h->comm);
   (void)hipFree(h->arena);
   (void)hipFree(h->d_ctr);
+  (void)hipFree(h->ones);
   (void)hipStreamSynchronize(h->act_stream);
   (void)hipStreamDestroy(h->act_stream);
   (void)hipEventDestroy(h->actor_ev);

@@ -74,7 +74,7 @@ def main():
                         print(f"   mark{k} {np.median(v[:, k] - v[:, 0]) * 0.01:5.2f}", end="")
                 print()
                 continue
-            if "gemm_kernel" not in kern and kern != "td3::dw_kernel":
+            if "gemm_kernel" not in kern and not kern.startswith("td3::dw_kernel"):
                 print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f}")
                 continue
             lib.td3_tl_clear()
