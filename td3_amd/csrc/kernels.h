@@ -179,6 +179,11 @@ struct DwArgs {
 // ------------------------------------------------------------------ launchers (kernels.hip)
 int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds_bytes,
                 Counters* bump, int bump_actor, hipStream_t s);
+// Two independent GEMM stages in one launch (stage 2's tile ids follow stage 1's); only the pairs
+// gemm2_supported() reports are instantiated.
+int gemm2_supported(int m1, int w1, int p1, int m2, int w2, int p2);
+int launch_gemm2(int m1, int w1, int p1, const GemmTable& t1, int nb1, int m2, int w2, int p2, const GemmTable& t2,
+                 int nb2, int Bp, int lds, hipStream_t s);
 int launch_rows(int kind, const GemmTable& t, int Bp, hipStream_t s);
 // Two row kinds in one launch: problems [0, n1) run kind1, [n1, nprob) kind2.
 int launch_rows2(int kind1, int kind2, int n1, const GemmTable& t, int Bp, hipStream_t s);

@@ -1106,11 +1106,10 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 #ifndef TD3_L0_LATE_B
 #define TD3_L0_LATE_B 0
 #endif
+// One workgroup's tile b of a GEMM stage (the body of gemm_kernel / gemm2_kernel).
 template <int MODE, int WN, int PRO>
-__global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
-                                                        GemmTable tab, Counters* bump, int bump_actor) {
-  extern __shared__ float4 smem4[];
-  float* smem = reinterpret_cast<float*>(smem4);
+__device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, int tb3, int Bp, const GemmTable& tab,
+                                          Counters* bump, int bump_actor, float* smem) {
   // WN = 0: 16 output columns per workgroup on v_mfma_f32_16x16x4_f32 (two 16-row halves of the
   // 32-row tile): half the MFMA chain of WN = 1 for stages of <= 128 32-column workgroups, which
   // otherwise leave half the CUs idle (td3.hip gemm_wn)
@@ -1119,9 +1118,6 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
   constexpr int NT = 64 * kNW;                 // threads
   constexpr int OUTW = WN == 0 ? 16 : 32 * WN; // output columns of the workgroup
   constexpr bool kPrefetchB = true;
-  const int b = xcd_tile(nb);
-  TL_MARK(0);
-  if (b >= nb) return;
   int pi = 0;
   if (nprob > 1 && b >= tb1) pi = 1;
   if (nprob > 2 && b >= tb2) pi = 2;
@@ -1395,6 +1391,46 @@ __global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb,
       bump->pw[2] *= bump->beta[2];
       bump->pw[3] *= bump->beta[3];
     }
+  }
+}
+
+template <int MODE, int WN, int PRO>
+__global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
+                                                        GemmTable tab, Counters* bump, int bump_actor) {
+  extern __shared__ float4 smem4[];
+  const int b = xcd_tile(nb);
+  TL_MARK(0);
+  if (b >= nb) return;
+  gemm_body<MODE, WN, PRO>(b, nprob, tb1, tb2, tb3, Bp, tab, bump, bump_actor, reinterpret_cast<float*>(smem4));
+}
+
+// Two independent GEMM stages in one launch (the unit-gradient critic backward beside the target
+// twin's forward, td3.hip): a uniform branch per workgroup picks the stage; the launch takes the
+// larger LDS and register footprint of the two bodies.
+// Tile placement: stage 1's tiles take the first 8*ceil(nb1/8) workgroup ids, dealt over the 8
+// XCDs as xcd_tile does (consecutive tiles, which share weight columns, on one XCD); stage 2's
+// follow the same way.  Dispatched in id order, stage 1 (the longer forward layer) gets a CU per
+// workgroup and stage 2 starts on the CUs it leaves free, refilling them as its workgroups end.
+#ifndef TD3_DUAL_OCC
+#define TD3_DUAL_OCC 4
+#endif
+template <int M1, int W1, int P1, int M2, int W2, int P2>
+__global__ __launch_bounds__(64 * kNW, (W1 == 4 || W2 == 4) ? 4 : TD3_DUAL_OCC) void gemm2_kernel(
+    int nb1, int nb2, int Bp, int np1, int a1, int a2, int a3, int np2, int c1, int c2, int c3, GemmTable t1,
+    GemmTable t2) {
+  extern __shared__ float4 smem4[];
+  TL_MARK(0);
+  const int per1 = (nb1 + 7) >> 3, per2 = (nb2 + 7) >> 3;
+  float* smem = reinterpret_cast<float*>(smem4);
+  const int id = (int)blockIdx.x;
+  if (id < 8 * per1) {
+    const int b = (id & 7) * per1 + (id >> 3);
+    if (b >= nb1) return;
+    gemm_body<M1, W1, P1>(b, np1, a1, a2, a3, Bp, t1, nullptr, 0, smem);
+  } else {
+    const int l = id - 8 * per1, b = (l & 7) * per2 + (l >> 3);
+    if (b >= nb2) return;
+    gemm_body<M2, W2, P2>(b, np2, c1, c2, c3, Bp, t2, nullptr, 0, smem);
   }
 }
 
@@ -1823,6 +1859,7 @@ constexpr int kDw64Depth = 2;                       // 64-row steps in flight (1
 template <bool SC>
 __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   __shared__ float sm[2 * 2 * 64 * kDw64S];         // [buf][operand][64 rows][kDw64S]
+  __shared__ float4 ssl4[2][16];                     // SC: [buf] the 64 rows' dZ scales
   const int b = xcd_tile(nb);
   if (b >= nb) return;
   int pi = 0;
@@ -1846,18 +1883,20 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   // kDw64Depth steps of 64 rows are in flight in registers (HBM latency > one step's 16 MFMAs)
   constexpr int D = kDw64Depth;
   float4 sg[D][2], su[D][2];
-  float ssc[D][2];
-  auto fetch = [&](int r0, float4 (&g)[2], float4 (&u)[2], float (&sc)[2]) {
+  float ssc[D];
+  // SC: the step's 64 row scales ride along with the operands (thread t loads row t & 63's, the
+  // first wave puts them in LDS) and scale the dZ operand at the MFMA (16 per lane half and step)
+  auto fetch = [&](int r0, float4 (&g)[2], float4 (&u)[2], float& sc) {
 #pragma unroll
     for (int v = 0; v < 2; ++v) {
       const int e = tid + 512 * v, row = r0 + (e >> 4), c4 = (e & 15) * 4;
       const bool live = row < a.Bp;
       g[v] = (live && n0 + c4 < P.Np) ? gld4(P.G + (size_t)row * P.ldg + n0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
       u[v] = (live && k0 + c4 < P.Kp) ? gld4(P.U + (size_t)row * P.ldu + k0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      sc[v] = SC ? gld(P.rs + (size_t)min(row, a.Bp - 1) * P.ldrs) : 1.f;   // dZ row scale (unit rows)
     }
+    if constexpr (SC) sc = gld(P.rs + (size_t)min(r0 + (tid & 63), a.Bp - 1) * P.ldrs);
   };
-  auto put = [&](int buf, const float4 (&gq)[2], const float4 (&uq)[2], const float (&sc)[2]) {
+  auto put = [&](int buf, const float4 (&gq)[2], const float4 (&uq)[2], float sc) {
     float* g = sm + buf * 2 * 64 * kDw64S;
     float* uu = g + 64 * kDw64S;
 #pragma unroll
@@ -1865,8 +1904,11 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
       const int e = tid + 512 * v, row = e >> 4, c4 = (e & 15) * 4;
       float* gp = g + row * kDw64S + c4;
       float* up = uu + row * kDw64S + c4;
-      gp[0] = gq[v].x * sc[v]; gp[1] = gq[v].y * sc[v]; gp[2] = gq[v].z * sc[v]; gp[3] = gq[v].w * sc[v];
+      gp[0] = gq[v].x; gp[1] = gq[v].y; gp[2] = gq[v].z; gp[3] = gq[v].w;
       up[0] = uq[v].x; up[1] = uq[v].y; up[2] = uq[v].z; up[3] = uq[v].w;
+    }
+    if constexpr (SC) {
+      if (tid < 64) reinterpret_cast<float*>(ssl4[buf])[tid] = sc;
     }
   };
   f32x16 acc;
@@ -1887,9 +1929,17 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
       if (st + D < nstep) fetch((st + D) * 64, sg[d], su[d], ssc[d]);
       const float* g = sm + buf * 2 * 64 * kDw64S + (rh * 32 + 16 * h) * kDw64S;
       const float* uu = g + 64 * kDw64S;
+      float scl[16];
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2)
-        acc = mfma32x32x2(g[s2 * kDw64S + qn * 32 + i], uu[s2 * kDw64S + qk * 32 + i], acc);
+      for (int q = 0; q < 4; ++q) {
+        const float4 v4 = SC ? ssl4[buf][(rh * 32 + 16 * h) / 4 + q] : make_float4(1.f, 1.f, 1.f, 1.f);
+        scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const float ga = g[s2 * kDw64S + qn * 32 + i];
+        acc = mfma32x32x2(SC ? ga * scl[s2] : ga, uu[s2 * kDw64S + qk * 32 + i], acc);
+      }
     }
   }
   __syncthreads();                                   // staging buffers become the reduction tile
@@ -1977,6 +2027,46 @@ static GemmFn pick_gemm(int mode, int wn, int pro) {
   if (mode == 1 && wn == 2) return pick_bwd<2>(pro);
   if (mode == 1 && wn == 4) return pick_bwd<4>(pro);
   return nullptr;
+}
+
+// The stage pairs the planner merges (td3.hip): {forward layer of the target twin} x {input-grad
+// stage of the unit critic backward} at the widths gemm_wn picks for B = 64..1024.
+#define TD3_GEMM2_PAIRS(X)                                            \
+  X(0, 1, kProL0, 1, 1, kProCopy) X(0, 0, kProLN, 1, 1, kProLNBwd)     \
+  X(0, 0, kProL0, 1, 0, kProCopy) X(0, 0, kProLN, 1, 0, kProLNBwd)     \
+  X(0, 4, kProL0, 1, 4, kProCopy) X(0, 1, kProLN, 1, 4, kProLNBwd)     \
+  X(0, 4, kProCopy, 1, 4, kProCopy) X(0, 4, kProLN, 1, 4, kProLNBwd)   \
+  X(0, 0, kProCopy, 1, 0, kProCopy) X(0, 1, kProL0, 1, 0, kProCopy)    \
+  X(0, 0, kProL0, 1, 1, kProCopy) X(0, 1, kProLN, 1, 1, kProLNBwd)
+
+int gemm2_supported(int m1, int w1, int p1, int m2, int w2, int p2) {
+#define TD3_G2_Q(A, B, C, D, E, F) \
+  if (m1 == A && w1 == B && p1 == C && m2 == D && w2 == E && p2 == F) return 1;
+  TD3_GEMM2_PAIRS(TD3_G2_Q)
+#undef TD3_G2_Q
+  return 0;
+}
+
+int launch_gemm2(int m1, int w1, int p1, const GemmTable& t1, int nb1, int m2, int w2, int p2, const GemmTable& t2,
+                 int nb2, int Bp, int lds, hipStream_t s) {
+  const dim3 grid(8 * (((nb1 + 7) >> 3) + ((nb2 + 7) >> 3)));
+  auto dir = [](const GemmTable& t, int n, int i) { return t.nprob > i ? t.p[i].tile_begin : n; };
+  bool done = false;
+#define TD3_G2_L(A, B, C, D, E, F)                                                                           \
+  if (!done && m1 == A && w1 == B && p1 == C && m2 == D && w2 == E && p2 == F) {                              \
+    hipLaunchKernelGGL((gemm2_kernel<A, B, C, D, E, F>), grid, dim3(64 * kNW), lds, s, nb1, nb2, Bp, t1.nprob, \
+                       dir(t1, nb1, 1), dir(t1, nb1, 2), dir(t1, nb1, 3), t2.nprob, dir(t2, nb2, 1),           \
+                       dir(t2, nb2, 2), dir(t2, nb2, 3), t1, t2);                                            \
+    done = true;                                                                                              \
+  }
+  TD3_GEMM2_PAIRS(TD3_G2_L)
+#undef TD3_G2_L
+  if (!done) {
+    set_error("launch_gemm2: stage pair (%d,%d,%d)+(%d,%d,%d) not instantiated", m1, w1, p1, m2, w2, p2);
+    return -1;
+  }
+  TD3_HIP(hipGetLastError());
+  return 0;
 }
 
 int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds,
@@ -2116,6 +2206,11 @@ static int set_attr_all() {
 }
 
 int kernels_init() {
+#define TD3_G2_A(A, B, C, D, E, F)                                                               \
+  TD3_HIP(hipFuncSetAttribute((const void*)gemm2_kernel<A, B, C, D, E, F>,                        \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  TD3_GEMM2_PAIRS(TD3_G2_A)
+#undef TD3_G2_A
   int rc = set_attr_all<0>();
   if (!rc) rc = set_attr_all<1>();
   if (!rc) rc = set_attr_all<2>();

@@ -154,11 +154,20 @@ struct Scratch {
   }
 };
 
+// A GEMM stage's launch, kept so the planner can merge two independent stages into one launch.
+struct GemmLaunch {
+  int mode, wn, pro;
+  GemmTable t;
+  int blocks, Bp, lds;
+  bool plain;           // no ring binding, no counter bump: mergeable
+};
+
 struct Stage {
   std::string name;
   std::function<int(hipStream_t)> run;
   double flops = 0;
   std::string kernel;   // HIP kernel function the stage launches (rocprof name)
+  std::shared_ptr<GemmLaunch> gemm;   // GEMM stages only
 };
 
 struct Plan {
@@ -334,7 +343,43 @@ static int push_gemm_stage(td3_handle* h, std::vector<void*>& owned, std::vector
   st.push_back({name,
                 [=](hipStream_t s) { return launch_gemm(mode, wn, pro, t, blocks, Bp, lds, bump, bump_actor, s); },
                 flops, kname});
+  st.back().gemm = std::make_shared<GemmLaunch>(GemmLaunch{mode, wn, pro, t, blocks, Bp, lds, bump == nullptr});
   return 0;
+}
+
+// Run GEMM stage j inside stage i's launch (i < j; stage j must depend on nothing in (i, j) and
+// nothing in (i, j) on it).  Forward stage first in the pair.  Left as two launches when the pair
+// is not instantiated (gemm2_supported) or either stage binds the ring / bumps the counters.
+#ifndef TD3_MERGE_GEMM_PAIRS
+#define TD3_MERGE_GEMM_PAIRS 1
+#endif
+static bool merge_gemm_pair(std::vector<Stage>& st, size_t i, size_t j) {
+  if (!TD3_MERGE_GEMM_PAIRS || i >= j || j >= st.size()) return false;
+  const std::shared_ptr<GemmLaunch> a0 = st[i].gemm, b0 = st[j].gemm;
+  if (!a0 || !b0 || !a0->plain || !b0->plain || a0->Bp != b0->Bp) return false;
+  const bool a_first = a0->mode == 0;
+  const GemmLaunch f = a_first ? *a0 : *b0, g = a_first ? *b0 : *a0;
+  if (!gemm2_supported(f.mode, f.wn, f.pro, g.mode, g.wn, g.pro)) return false;
+  Stage m;
+  m.name = st[i].name + "+" + st[j].name;
+  m.flops = st[i].flops + st[j].flops;
+  char kname[96];
+  snprintf(kname, sizeof(kname), "td3::gemm2_kernel<%d, %d, %d, %d, %d, %d>", f.mode, f.wn, f.pro, g.mode, g.wn,
+           g.pro);
+  m.kernel = kname;
+  const int lds = std::max(f.lds, g.lds);
+  m.run = [=](hipStream_t s) {
+    return launch_gemm2(f.mode, f.wn, f.pro, f.t, f.blocks, g.mode, g.wn, g.pro, g.t, g.blocks, f.Bp, lds, s);
+  };
+  st[i] = m;
+  st.erase(st.begin() + (long)j);
+  return true;
+}
+
+static int stage_index(const std::vector<Stage>& st, const std::string& name) {
+  for (size_t k = 0; k < st.size(); ++k)
+    if (st[k].name == name) return (int)k;
+  return -1;
 }
 
 static int push_row_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
@@ -502,8 +547,10 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.tile_begin = blocks;
       blocks += (Bp / 32) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
-      // fused layer 0: + the staged input rows and the H0 rows kept for the sliced store
-      lds = std::max(lds, gemm_lds_bytes(L.Kp) + (l0 ? 32 * kL0XS * 4 + 32 * lds_stride(L.Kp) * 4 : 0));
+      // fused layer 0: + the staged input rows and (networks with a backward, norm on: l0_mfma's
+      // `keep`) the H0 rows kept for the sliced store
+      const bool keep_h0 = l0 && norm && it.stats;
+      lds = std::max(lds, gemm_lds_bytes(L.Kp) + (l0 ? 32 * kL0XS * 4 : 0) + (keep_h0 ? 32 * lds_stride(L.Kp) * 4 : 0));
       if (l0) flops += 2.0 * Bp * it.net->lin[0].N * it.net->lin[0].K;
       probs.push_back(p);
     }
@@ -975,6 +1022,17 @@ static int build_step(td3_handle* h, int B) {
         TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true, false, &rows));
         std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
         TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, nullptr, nullptr, 0, true));
+        {   // the unit backward's input-grad stages share launches with the target twin's layers, in
+            // order: TF layer k moves up to CB stage k only while every earlier TF layer moved too
+          const char* cbn[2] = {"CB_bwd2", "CB_bwd1"};
+          std::vector<std::string> tfn;
+          for (const char* n : {"TF_fwd0", "TF_fwd01", "TF_fwd1", "TF_fwd2"})
+            if (stage_index(st, n) >= 0) tfn.push_back(n);
+          for (size_t k = 0; k < 2 && k < tfn.size(); ++k) {
+            const int i = stage_index(st, cbn[k]), j = stage_index(st, tfn[k]);
+            if (i < 0 || j <= i || !merge_gemm_pair(st, (size_t)i, (size_t)j)) break;
+          }
+        }
         TD3_RC(push_row2_stage(st, rows, kRowTargetLoss, kRowLnBwd, 1, Bp, "critic_loss"));
         const std::vector<const float*> usc = {P->gscale[0], P->gscale[1]};
         TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, 0, &usc));
