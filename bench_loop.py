@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--env-cost-us", type=float, default=50.0)
+    ap.add_argument("--use-graph", type=int, choices=(0, 1, 2), default=2,
+                    help="td3_config.use_graph: 0 direct launches, 1 graph replays, 2 auto (default)")
     args = ap.parse_args()
     from td3_amd.TD3_featured import TD3
     from td3_amd.my_replay_buffer import ReplayBuffer_featured
@@ -64,7 +66,8 @@ def main():
     for mode in ("overlap", "serial"):
         np.random.seed(0)
         env = SyntheticEnv(sd, ad, max_action=ma, max_episode_steps=1000, step_cost_us=args.env_cost_us)
-        pol = TD3(env.observation_space, env.action_space, max_action=ma, norm="layer")
+        pol = TD3(env.observation_space, env.action_space, max_action=ma, norm="layer",
+                  use_graph={0: False, 1: True, 2: "auto"}[args.use_graph])
         rb = ReplayBuffer_featured(env.observation_space, env.action_space, max_size=1_000_000)
         rb.fill_synthetic(100_000, max_action=ma, seed=1)
         p = pol if mode == "overlap" else _SerialPolicy(pol)
@@ -88,7 +91,7 @@ def main():
         "value": round(out["overlap"], 1), "unit": "env-steps/s", "higher_is_better": True,
         "serial_value": round(out["serial"], 1), "speedup_vs_serial": round(out["overlap"] / out["serial"], 3),
         "env_only_steps_per_s": round(host_only, 1), "env_cost_us": args.env_cost_us,
-        "steps": args.steps, "warmup": args.warmup, "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "n_gpus": 1, "use_graph": args.use_graph,
         "data": "SyntheticEnv (tanh linear dynamics + busy-wait per step), replay ring pre-filled with 1e5 "
                 "synthetic rows, one train per env step"}))
 

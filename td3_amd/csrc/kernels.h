@@ -131,6 +131,35 @@ struct HeadArgs {
   int gen_noise;
 };
 
+// ------------------------------------------------------------------ small-query hidden layers
+// select_action / eval_q of up to kGemvRows query rows: each hidden Linear as wave dot products
+// (a 32-row MFMA tile would compute 31 pad rows, each workgroup walking K serially).
+constexpr int kGemvRows = 4;
+struct GemvProb {
+  const float* X; int ldx; int K;       // input rows: the query, or the previous layer's ReLU output
+  const float* lng; const float* lnb;   // LayerNorm of the input (nullable: layer 0 / norm=None)
+  const float* W; int ldw; const float* b; int N;
+  float* Y; int ldy;                    // Y[r][o] = relu(LN(X[r]) . W[o] + b[o]), o < N
+};
+struct GemvArgs {
+  GemvProb p[2];                        // one per network (eval_q: the twin's two)
+  int B;                                // live rows, 1..kGemvRows
+};
+int launch_gemv(const GemvArgs& a, int nprob, hipStream_t s);
+
+// Layers 0 and 1 in one launch, for a layer 0 of at most kGemv0K inputs (the featured state /
+// state-action row): every workgroup computes all of H0 = relu(W0 x + b0) into LDS (W0 is small),
+// then its layer-1 columns as gemv_kernel.  The query rows travel in the kernel arguments.
+constexpr int kGemv0K = 64;
+constexpr int kGemvQ = kGemvRows * kGemv0K + 4;
+struct Gemv01Args {
+  GemvArgs l1;                          // layer 1 (its X is unused) and the live rows B
+  const float* W0[2]; const float* b0[2];
+  int ldw0, K0, N0;                     // the same shapes for both networks (twin critics)
+  float xq[kGemvQ];                     // query rows [B][K0], zero past B*K0
+};
+int launch_gemv01(const Gemv01Args& a, int nprob, hipStream_t s);
+
 // dZ = relu'(LN_bwd(dU)) on full rows (layer 0, where no GEMM follows).
 struct LnBwdProb {
   const float* GU; const float* H; const float* stats; const float* lng; int ld, K;

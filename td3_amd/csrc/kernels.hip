@@ -1472,6 +1472,111 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   }
 }
 
+// ================================================================== small-query hidden layers
+// One wave per 4 output columns of one network (blockIdx.y): the wave loads its 4 weight rows
+// and the R query rows (lane-sliced, K <= 512), applies the input LayerNorm (the GEMM prologue's
+// packed form: pads of X, gamma, beta are zero) and reduces the 4R dot products.
+template <int R>
+__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
+  const GemvProb& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int o0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+  if (o0 >= P.N) return;
+  float w[4][8], x[R][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rv_load(w[j], P.W + (size_t)min(o0 + j, P.N - 1) * P.ldw, P.K, lane);
+#pragma unroll
+  for (int r = 0; r < R; ++r) rv_load(x[r], P.X + (size_t)min(r, a.B - 1) * P.ldx, P.K, lane);
+  if (P.lng) {
+    float g[8], bb[8], rm[8], mean[R], rstd[R];
+    rv_load(g, P.lng, P.K, lane);
+    rv_load(bb, P.lnb, P.K, lane);
+    real_mask(rm, P.K, lane);
+    ln_fwd_rows_pk<R>(x, g, bb, rm, 1.0f / (float)P.K, mean, rstd);
+  }
+  float z[4][R];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < R; ++r) z[j][r] = wsum(rv_pdot(x[r], w[j], P.K, lane));
+  // lane 4r + j stores column o0 + j of row r
+  const int j = lane & 3, r = lane >> 2;
+  if (r < R && r < a.B && o0 + j < P.N) {
+    float v = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr)
+        if (jj == j && rr == r) v = z[jj][rr];
+    gst(P.Y + (size_t)r * P.ldy + o0 + j, fmaxf(v + gld(P.b + o0 + j), 0.f));
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void gemv01_kernel(Gemv01Args a) {
+  __shared__ float h0[R][512];
+  const GemvProb& P = a.l1.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int o0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+  float w[4][8], x[R][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rv_load(w[j], P.W + (size_t)min(o0 + j, P.N - 1) * P.ldw, P.K, lane);
+  // H0 (all N0 columns, zero pads) into LDS; W0 pads past K0 are zero, so the float4 steps may
+  // read past a row's K0 query values (xq is zero past B*K0 and padded by 4)
+  const float* W0 = a.W0[blockIdx.y];
+  const float* b0 = a.b0[blockIdx.y];
+  for (int o = threadIdx.x; o < 512; o += 256) {
+    float z[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) z[r] = 0.f;
+    if (o < a.N0) {
+      const float* wr = W0 + (size_t)o * a.ldw0;
+      for (int c = 0; c < a.K0; c += 4) {
+        const float4 wv = gld4(wr + c);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const float* q = a.xq + r * a.K0 + c;
+          z[r] += wv.x * q[0];
+          z[r] += wv.y * q[1];
+          z[r] += wv.z * q[2];
+          z[r] += wv.w * q[3];
+        }
+      }
+      const float bo = gld(b0 + o);
+#pragma unroll
+      for (int r = 0; r < R; ++r) z[r] = fmaxf(z[r] + bo, 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) h0[r][o] = z[r];
+  }
+  __syncthreads();
+  if (o0 >= P.N) return;
+#pragma unroll
+  for (int r = 0; r < R; ++r) rv_load_lds(x[r], h0[r], P.K, lane);
+  if (P.lng) {
+    float g[8], bb[8], rm[8], mean[R], rstd[R];
+    rv_load(g, P.lng, P.K, lane);
+    rv_load(bb, P.lnb, P.K, lane);
+    real_mask(rm, P.K, lane);
+    ln_fwd_rows_pk<R>(x, g, bb, rm, 1.0f / (float)P.K, mean, rstd);
+  }
+  float z[4][R];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < R; ++r) z[j][r] = wsum(rv_pdot(x[r], w[j], P.K, lane));
+  const int j = lane & 3, r = lane >> 2;
+  if (r < R && r < a.l1.B && o0 + j < P.N) {
+    float v = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr)
+        if (jj == j && rr == r) v = z[jj][rr];
+    gst(P.Y + (size_t)r * P.ldy + o0 + j, fmaxf(v + gld(P.b + o0 + j), 0.f));
+  }
+}
+
 // templated on NORM and with the problems in the kernel arguments: a runtime `norm` select on
 // the statistics loads compiled to a branch and a load drain per row (5 dependent load rounds)
 #ifndef TD3_LNBWD_RB
@@ -2144,6 +2249,48 @@ int launch_rows2(int kind1, int kind2, int n1, const GemmTable& d, int Bp, hipSt
 
 int launch_heads(const HeadArgs& a, int nprob, hipStream_t s) {
   hipLaunchKernelGGL(head_kernel, dim3(a.Bp / 4, nprob), dim3(256), 0, s, a);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_gemv(const GemvArgs& a, int nprob, hipStream_t s) {
+  int N = 0;
+  for (int k = 0; k < nprob; ++k) N = std::max(N, a.p[k].N);
+  if (nprob < 1 || nprob > 2 || a.B < 1 || a.B > kGemvRows) {
+    set_error("launch_gemv: %d problems (max 2), %d rows (max %d)", nprob, a.B, kGemvRows);
+    return -1;
+  }
+  for (int k = 0; k < nprob; ++k)
+    if (a.p[k].K > 512 || a.p[k].K < 1) {
+      set_error("launch_gemv: input width %d (max 512)", a.p[k].K);
+      return -1;
+    }
+  const dim3 grid((N + 15) / 16, nprob);
+  if (a.B == 1) hipLaunchKernelGGL(gemv_kernel<1>, grid, dim3(256), 0, s, a);
+  else if (a.B == 2) hipLaunchKernelGGL(gemv_kernel<2>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(gemv_kernel<4>, grid, dim3(256), 0, s, a);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_gemv01(const Gemv01Args& a, int nprob, hipStream_t s) {
+  int N = 0;
+  for (int k = 0; k < nprob; ++k) N = std::max(N, a.l1.p[k].N);
+  if (nprob < 1 || nprob > 2 || a.l1.B < 1 || a.l1.B > kGemvRows || a.K0 < 1 || a.K0 > kGemv0K ||
+      a.N0 > 512 || a.N0 < 1) {
+    set_error("launch_gemv01: %d problems, %d rows, layer 0 %d -> %d (max 2, %d, %d -> 512)", nprob, a.l1.B, a.K0,
+              a.N0, kGemvRows, kGemv0K);
+    return -1;
+  }
+  for (int k = 0; k < nprob; ++k)
+    if (a.l1.p[k].K != a.N0 || a.l1.p[k].K > 512) {
+      set_error("launch_gemv01: layer-1 input width %d != layer-0 width %d", a.l1.p[k].K, a.N0);
+      return -1;
+    }
+  const dim3 grid((N + 15) / 16, nprob);
+  if (a.l1.B == 1) hipLaunchKernelGGL(gemv01_kernel<1>, grid, dim3(256), 0, s, a);
+  else if (a.l1.B == 2) hipLaunchKernelGGL(gemv01_kernel<2>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(gemv01_kernel<4>, grid, dim3(256), 0, s, a);
   TD3_HIP(hipGetLastError());
   return 0;
 }

@@ -28,10 +28,13 @@ struct Ring {
   int device = 0;
   hipStream_t stream = nullptr;
   float* stage[2] = {nullptr, nullptr};     // pinned host staging for add(), double-buffered
+  float* stage_dev[2] = {nullptr, nullptr}; // their device addresses (small adds read them in place)
   size_t stage_cap[2] = {0, 0};
-  hipEvent_t stage_buf_ev[2] = {nullptr, nullptr};  // H2D out of stage[i] finished
+  hipEvent_t stage_buf_ev[2] = {nullptr, nullptr};  // the write out of stage[i] finished
   int stage_cur = 0;
-  hipEvent_t stage_ev = nullptr;   // the last write (records + d_size): readers wait on it
+  hipEvent_t stage_ev = nullptr;   // recorded after writes that use no staging buffer
+  hipEvent_t last_write = nullptr; // the last write (records + d_size), stage_ev or a stage_buf_ev:
+                                   // readers wait on it
   // Ordering of writes after reads.  Every reader (a learner step, a stand-alone sample) records
   // read_ev on its stream after the work that reads the records or d_size; a later write waits on
   // it, so a step in flight never sees d_size or a record change under it.  Readers on different

@@ -111,8 +111,24 @@ __global__ __launch_bounds__(256) void fill_kernel(float* data, int rec, int o_a
 
 __global__ void set_i64_kernel(int64_t* p, int64_t v) { *p = v; }
 
+// Small adds: n staged records, read in place from mapped pinned host memory, into the ring rows
+// ptr, ptr+1, ... (wrapping), and the new size -- one launch instead of a DMA copy per ring
+// segment plus the size update.  rec is a multiple of 4 (replay.h), so records move as float4.
+__global__ __launch_bounds__(256) void ring_put_kernel(float4* __restrict__ data, int64_t cap, int rec4,
+                                                       const float4* __restrict__ src, int64_t n, int64_t ptr,
+                                                       int64_t* d_size, int64_t new_size) {
+  const int64_t total = n * rec4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / rec4, c = i - row * rec4;
+    int64_t dst = ptr + row;
+    if (dst >= cap) dst -= cap;
+    data[dst * rec4 + c] = src[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *d_size = new_size;
+}
+
 int ring_begin_read(Ring* r, hipStream_t s) {
-  TD3_HIP(hipStreamWaitEvent(s, r->stage_ev, 0));
+  TD3_HIP(hipStreamWaitEvent(s, r->last_write, 0));
   if (r->read_stream && r->read_stream != (const void*)s) TD3_HIP(hipStreamWaitEvent(s, r->read_ev, 0));
   return 0;
 }
@@ -152,6 +168,7 @@ static int ring_alloc(Ring* r, int64_t max_size, int device, uint64_t seed, rb_h
   TD3_HIP(hipDeviceSynchronize());
   TD3_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
   TD3_HIP(hipEventCreateWithFlags(&r->stage_ev, hipEventDisableTiming));
+  r->last_write = r->stage_ev;
   TD3_HIP(hipEventCreateWithFlags(&r->read_ev, hipEventDisableTiming));
   for (auto& ev : r->stage_buf_ev) TD3_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   *out = reinterpret_cast<rb_handle*>(r);
@@ -252,20 +269,23 @@ static float* ensure_stage(Ring* r, size_t floats) {
     r->stage[i] = nullptr;
     r->stage_cap[i] = 0;
     const size_t cap = std::max(floats, (size_t)r->rec * 4096);
-    hipError_t e = hipHostMalloc(&r->stage[i], cap * sizeof(float), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&r->stage[i], cap * sizeof(float), hipHostMallocMapped);
+    void* d = nullptr;
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&d, r->stage[i], 0);
     if (e != hipSuccess) {
       set_error("rb_add: hipHostMalloc(%zu bytes) failed: %s", cap * sizeof(float), hipGetErrorString(e));
       return nullptr;
     }
+    r->stage_dev[i] = static_cast<float*>(d);
     r->stage_cap[i] = cap;
   }
   return r->stage[i];
 }
 
-static hipEvent_t stage_event_of(Ring* r, const float* host) {
+static int stage_index(const Ring* r, const float* host) {
   for (int i = 0; i < 2; ++i)
-    if (host == r->stage[i]) return r->stage_buf_ev[i];
-  return nullptr;
+    if (host == r->stage[i]) return i;
+  return -1;
 }
 
 // Writes (records, d_size) on `stream` start after every read queued so far (Ring::read_ev).
@@ -275,37 +295,54 @@ static int ring_begin_write(Ring* r, hipStream_t stream) {
   return 0;
 }
 
-static int ring_end_write(Ring* r, hipStream_t stream) {
-  TD3_HIP(hipEventRecord(r->stage_ev, stream));
+// `ev`: the event that marks this write (a staging buffer's, which then also frees the buffer),
+// or nullptr for the ring's own.
+static int ring_end_write(Ring* r, hipStream_t stream, hipEvent_t ev = nullptr) {
+  if (!ev) ev = r->stage_ev;
+  TD3_HIP(hipEventRecord(ev, stream));
+  r->last_write = ev;
   return 0;
 }
+
+constexpr size_t kPutKernelBytes = 256 << 10;   // adds up to this size take ring_put_kernel
 
 // Copy n packed records (host staging) into the ring at ptr, wrapping (the ring
 // semantics of my_replay_buffer.py:115-116 applied n times).
 static int push_staged(Ring* r, const float* host, int64_t n, hipStream_t stream) {
   TD3_RC(ring_begin_write(r, stream));
+  const int si = stage_index(r, host);
   int64_t done = 0;
   // Only the last `cap` records survive when n > cap.
-  const float* src = host;
+  int64_t skip = 0;
   if (n > r->cap) {
-    int64_t skip = n - r->cap;
+    skip = n - r->cap;
     r->ptr = (r->ptr + skip) % r->cap;
-    src += (size_t)skip * r->rec;
     n = r->cap;
     r->size = r->cap;
   }
-  while (done < n) {
-    int64_t chunk = std::min<int64_t>(n - done, r->cap - r->ptr);
-    TD3_HIP(hipMemcpyAsync(r->data + (size_t)r->ptr * r->rec, src + (size_t)done * r->rec,
-                           (size_t)chunk * r->rec * sizeof(float), hipMemcpyHostToDevice, stream));
-    r->ptr = (r->ptr + chunk) % r->cap;
-    done += chunk;
+  const int64_t new_size = std::min<int64_t>(r->size + n, r->cap);
+  if (si >= 0 && (size_t)n * r->rec * sizeof(float) <= kPutKernelBytes) {
+    const int64_t total4 = n * (r->rec / 4);
+    const int grid = (int)std::min<int64_t>((total4 + 255) / 256, 256);
+    hipLaunchKernelGGL(ring_put_kernel, dim3(grid), dim3(256), 0, stream, reinterpret_cast<float4*>(r->data),
+                       r->cap, r->rec / 4, reinterpret_cast<const float4*>(r->stage_dev[si] + (size_t)skip * r->rec),
+                       n, r->ptr, r->d_size, new_size);
+    TD3_HIP(hipGetLastError());
+    r->ptr = (r->ptr + n) % r->cap;
+  } else {
+    const float* src = host + (size_t)skip * r->rec;
+    while (done < n) {
+      int64_t chunk = std::min<int64_t>(n - done, r->cap - r->ptr);
+      TD3_HIP(hipMemcpyAsync(r->data + (size_t)r->ptr * r->rec, src + (size_t)done * r->rec,
+                             (size_t)chunk * r->rec * sizeof(float), hipMemcpyHostToDevice, stream));
+      r->ptr = (r->ptr + chunk) % r->cap;
+      done += chunk;
+    }
+    hipLaunchKernelGGL(set_i64_kernel, dim3(1), dim3(1), 0, stream, r->d_size, new_size);
+    TD3_HIP(hipGetLastError());
   }
-  r->size = std::min<int64_t>(r->size + n, r->cap);
-  hipLaunchKernelGGL(set_i64_kernel, dim3(1), dim3(1), 0, stream, r->d_size, r->size);
-  TD3_HIP(hipGetLastError());
-  if (hipEvent_t be = stage_event_of(r, host)) TD3_HIP(hipEventRecord(be, stream));
-  return ring_end_write(r, stream);
+  r->size = new_size;
+  return ring_end_write(r, stream, si >= 0 ? r->stage_buf_ev[si] : nullptr);
 }
 
 int rb_add(rb_handle* h, const double* state, const double* action, const double* next_state,

@@ -212,16 +212,62 @@ struct Plan {
   int nwg_a = 0;                        // ... for the actor's encoder (one network per launch)
 };
 
+// Query batches up to this many (padded) rows keep their inputs and outputs in mapped pinned host
+// memory that the stages read and write in place: an idle select_action is then the launch chain
+// and one stream sync, without the two copy commands (~10 + ~25 us on the host for pageable
+// copies, tools/api_cost.hip).  Larger batches use device buffers and DMA copies.
+constexpr int kMappedRows = 256;
+
 struct ActPlan {       // select_action / eval_q at small batch
   int Bp = 0;
   float* scratch = nullptr;
-  float *X_S = nullptr, *X_SA = nullptr, *X_SP = nullptr;
-  float *XQ2 = nullptr, *pbatch = nullptr, *out = nullptr;   // particles
+  float* hio = nullptr;  // mapped pinned block (Bp <= kMappedRows), else nullptr
+  // device addresses the stages use; the h* twins are their host views when mapped
+  float *X_S = nullptr, *X_SA = nullptr, *out = nullptr, *q[2] = {nullptr, nullptr};
+  float *XQ2 = nullptr, *pbatch = nullptr;   // particles
+  float *hX_S = nullptr, *hX_SA = nullptr, *hout = nullptr, *hq[2] = {nullptr, nullptr};
+  float *hXQ2 = nullptr, *hpbatch = nullptr;
+  int ldo = 0;           // row stride of `out`
+  // featured queries of n <= kGemvRows rows: hidden layers as gemv_kernel launches, then the head
+  bool gemv = false, gemv01 = false;
+  GemvArgs gv_act[3], gv_q[3];
+  Gemv01Args g01_act{}, g01_q{};
+  HeadArgs head_act{}, head_q{};
   int64_t* d_iota = nullptr;
   EvalB A, Q[2];
   std::vector<void*> tables;
   std::vector<Stage> act, evalq;
 };
+
+// Carves an ActPlan's query inputs / outputs from the mapped block, or from the device scratch.
+struct IoCarve {
+  Scratch* S;
+  float* h = nullptr;   // host view of the mapped block
+  float* d = nullptr;   // its device address
+  size_t used = 0;
+  float* take(size_t floats, float** host) {
+    if (!h) {
+      *host = nullptr;
+      return S->take(floats);
+    }
+    const size_t n = (floats + 63) & ~(size_t)63;
+    *host = h + used;
+    float* p = d + used;
+    used += n;
+    return p;
+  }
+};
+
+static int map_io(ActPlan* A, size_t floats, IoCarve* io) {
+  if (A->Bp > kMappedRows) return 0;
+  TD3_HIP(hipHostMalloc(&A->hio, floats * 4, hipHostMallocMapped));
+  memset(A->hio, 0, floats * 4);
+  void* d = nullptr;
+  TD3_HIP(hipHostGetDevicePointer(&d, A->hio, 0));
+  io->h = A->hio;
+  io->d = static_cast<float*>(d);
+  return 0;
+}
 
 }  // namespace td3
 
@@ -1636,7 +1682,8 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
   // Data parallel (RCCL comm attached): auto launches directly, so every rank issues its
   // all-reduces the same way whatever its local progress (no captured / uncaptured mix).
   const bool graph = h->cfg.use_graph == 1 ||
-                     (h->cfg.use_graph == 2 && !h->comm && hipEventQuery(h->actor_ev) != hipErrorNotReady);
+                     (h->cfg.use_graph == 2 && !h->comm && !actor_phase &&
+                      hipEventQuery(h->actor_ev) != hipErrorNotReady);
   if (!graph) {
     if (ring && !fused) TD3_RC(input_from_ring(h, ring, P, false, s));
     return run_stages(st, s);
@@ -1766,18 +1813,60 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[1];
   const int lds_s = pad32(h->sd), lds_sa = pad32(h->sd + h->ad);
-  size_t floats = (size_t)Bp * (lds_s + 2 * lds_sa) + eval_floats(an, Bp, false, norm) +
-                  2 * eval_floats(q1, Bp, false, norm) + 4096;
+  const size_t io_floats = (size_t)Bp * (lds_s + lds_sa + h->ad + 2) + 4 * 64;
+  size_t floats = io_floats + eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, false, norm) + 4096;
   TD3_HIP(hipMalloc(&A->scratch, floats * 4));
   TD3_HIP(hipMemset(A->scratch, 0, floats * 4));
   TD3_HIP(hipDeviceSynchronize());
   Scratch S{A->scratch, floats, 0};
-  A->X_S = S.take((size_t)Bp * lds_s);
-  A->X_SA = S.take((size_t)Bp * lds_sa);
-  A->X_SP = S.take((size_t)Bp * lds_sa);
+  IoCarve io{&S};
+  TD3_RC(map_io(A.get(), io_floats, &io));
+  A->X_S = io.take((size_t)Bp * lds_s, &A->hX_S);
+  A->X_SA = io.take((size_t)Bp * lds_sa, &A->hX_SA);
+  A->out = io.take((size_t)Bp * h->ad, &A->hout);
+  A->ldo = h->ad;
+  for (int j = 0; j < 2; ++j) A->q[j] = io.take(Bp, &A->hq[j]);
   alloc_eval(S, an, Bp, A->X_S, lds_s, false, norm, true, A->A);
   alloc_eval(S, q1, Bp, A->X_SA, lds_sa, false, norm, true, A->Q[0]);
   alloc_eval(S, q2, Bp, A->X_SA, lds_sa, false, norm, true, A->Q[1]);
+  auto gemv_layer = [&](const NetL& n, const float* Pp, const EvalB& e, int l) {
+    GemvProb g{};
+    g.X = l ? e.H[l - 1] : e.X;
+    g.ldx = l ? n.lin[l - 1].Np : e.ldx;
+    g.K = n.lin[l].K;
+    g.lng = (l && norm) ? Pp + n.ln[l - 1].offg : nullptr;
+    g.lnb = (l && norm) ? Pp + n.ln[l - 1].offb : nullptr;
+    g.W = Pp + n.lin[l].offW;
+    g.ldw = n.lin[l].Kp;
+    g.b = Pp + n.lin[l].offb;
+    g.N = n.lin[l].N;
+    g.Y = e.H[l];
+    g.ldy = n.lin[l].Np;
+    return g;
+  };
+  A->gemv = true;
+  for (int l = 0; l < 3; ++l) {
+    A->gv_act[l].p[0] = gemv_layer(an, h->actor.P, A->A, l);
+    A->gv_q[l].p[0] = gemv_layer(q1, h->critic.P, A->Q[0], l);
+    A->gv_q[l].p[1] = gemv_layer(q2, h->critic.P, A->Q[1], l);
+    for (const NetL* n : {&an, &q1, &q2}) A->gemv = A->gemv && n->lin[l].K <= 512;
+  }
+  A->gemv01 = A->gemv && an.lin[0].K <= kGemv0K && q1.lin[0].K <= kGemv0K;
+  auto g01 = [&](Gemv01Args& g, const GemvArgs& l1, std::initializer_list<const NetL*> nets, const float* Pp) {
+    g = Gemv01Args{};
+    g.l1 = l1;
+    int k = 0;
+    for (const NetL* n : nets) {
+      g.W0[k] = Pp + n->lin[0].offW;
+      g.b0[k] = Pp + n->lin[0].offb;
+      g.ldw0 = n->lin[0].Kp;
+      g.K0 = n->lin[0].K;
+      g.N0 = n->lin[0].N;
+      ++k;
+    }
+  };
+  g01(A->g01_act, A->gv_act[1], {&an}, h->actor.P);
+  g01(A->g01_q, A->gv_q[1], {&q1, &q2}, h->critic.P);
   auto head = [&](const NetL& n, const float* Pp, EvalB& e, int mode) {
     HeadProb q{};
     q.H3 = e.H[2];
@@ -1796,9 +1885,9 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     std::vector<FwdItem> f = {{&an, h->actor.P, &A->A, false, false}};
     TD3_RC(add_fwd_stages(h, A->tables, A->act, f, Bp, Bp, "act", nullptr, 0));
     HeadProb p = head(an, h->actor.P, A->A, kHeadPolicy);
-    p.out = A->X_SP;
-    p.ldo = lds_sa;
-    p.out_col = h->sd;
+    p.out = A->out;
+    p.ldo = A->ldo;
+    p.out_col = 0;
     p.tanh_out = A->A.T;
     void* d = nullptr;
     TD3_RC(upload(h, A->tables, &p, sizeof(p), &d));
@@ -1807,6 +1896,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     a.B = Bp;
     a.Bp = Bp;
     a.max_action = h->cfg.max_action;
+    A->head_act = a;
     A->act.push_back({"act_head", [=](hipStream_t s) { return launch_heads(a, 1, s); }, 0});
   }
   {
@@ -1816,7 +1906,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     std::vector<HeadProb> hp;
     for (int j = 0; j < 2; ++j) {
       HeadProb p = head(j ? q2 : q1, h->critic.P, A->Q[j], kHeadQ);
-      p.out = A->Q[j].Qv;
+      p.out = A->q[j];
       p.ldo = 1;
       hp.push_back(p);
     }
@@ -1827,6 +1917,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     a.B = Bp;
     a.Bp = Bp;
     a.max_action = h->cfg.max_action;
+    A->head_q = a;
     A->evalq.push_back({"evq_head", [=](hipStream_t s) { return launch_heads(a, 2, s); }, 0});
   }
   *out = A.get();
@@ -1851,17 +1942,22 @@ static int build_act_particles(td3_handle* h, int Bp, ActPlan** out) {
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[cdq ? 1 : 0];
   const int lda = an.lin[0].Kp, ldq = q1.lin[0].Kp;
-  size_t floats = (size_t)Bp * (lda + 2 * ldq) + (size_t)Bp * N * D + (size_t)Bp * 32 + 2 * (size_t)Bp +
-                  eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, false, norm) + 8192;
+  const size_t io_floats = (size_t)Bp * (lda + 2 * ldq + (size_t)N * D + 32 + 2 * 32) + 8 * 64;
+  size_t floats = io_floats + 2 * (size_t)Bp + eval_floats(an, Bp, false, norm) +
+                  2 * eval_floats(q1, Bp, false, norm) + 8192;
   TD3_HIP(hipMalloc(&A->scratch, floats * 4));
   TD3_HIP(hipMemset(A->scratch, 0, floats * 4));
   TD3_HIP(hipDeviceSynchronize());
   Scratch S{A->scratch, floats, 0};
-  A->X_S = S.take((size_t)Bp * lda);
-  A->X_SA = S.take((size_t)Bp * ldq);
-  A->XQ2 = S.take((size_t)Bp * ldq);
-  A->pbatch = S.take((size_t)Bp * N * D);
-  A->out = S.take((size_t)Bp * 32);
+  IoCarve io{&S};
+  TD3_RC(map_io(A.get(), io_floats, &io));
+  A->X_S = io.take((size_t)Bp * lda, &A->hX_S);
+  A->X_SA = io.take((size_t)Bp * ldq, &A->hX_SA);
+  A->XQ2 = io.take((size_t)Bp * ldq, &A->hXQ2);
+  A->pbatch = io.take((size_t)Bp * N * D, &A->hpbatch);
+  A->out = io.take((size_t)Bp * 32, &A->hout);
+  A->ldo = 32;
+  for (int j = 0; j < 2; ++j) A->q[j] = io.take((size_t)Bp * 32, &A->hq[j]);
   A->d_iota = (int64_t*)S.take(2 * (size_t)Bp);
   alloc_eval(S, an, Bp, A->X_S, lda, false, norm, true, A->A);
   alloc_eval(S, q1, Bp, A->X_SA, ldq, false, norm, true, A->Q[0]);
@@ -1928,7 +2024,7 @@ static int build_act_particles(td3_handle* h, int Bp, ActPlan** out) {
     std::vector<HeadProb> hp;
     for (int j = 0; j < (cdq ? 2 : 1); ++j) {
       HeadProb p = head(j ? q2 : q1, Pq, A->Q[j], kHeadQ);
-      p.out = A->Q[j].Qv;
+      p.out = A->q[j];
       p.ldo = 32;
       hp.push_back(p);
     }
@@ -2087,10 +2183,12 @@ int td3_destroy(td3_handle* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->cfg.device);
   (void)hipStreamSynchronize(h->stream);
+  (void)hipStreamSynchronize(h->act_stream);
   if (h->plan) destroy_plan(h->plan.get());
   for (auto& kv : h->act) {
     free_plan_tables(kv.second->tables);
     (void)hipFree(kv.second->scratch);
+    if (kv.second->hio) (void)hipHostFree(kv.second->hio);
   }
   if (h->comm) ncclCommDestroy(h->comm);
   (void)hipFree(h->arena);
@@ -2297,6 +2395,58 @@ int td3_train_step_batch(td3_handle* h, const float* state, const float* action,
   return finish_step(h, actor_phase, s, stats);
 }
 
+// Host-side query I/O of an ActPlan: rows into the plan's inputs / outputs out to the caller.
+// Mapped plans (Bp <= kMappedRows) are written and read in place by the host; the stream is idle
+// when they are touched (every query ends in a sync, and one starts with it in case an earlier
+// query failed before its own).
+static int put_rows(const ActPlan* A, float* dev, float* host, int ld, int col, const float* src, int n, int cols,
+                    hipStream_t s) {
+  if (!host) return copy_rows_h2d(dev, ld, col, src, n, cols, s);
+  for (int i = 0; i < n; ++i) memcpy(host + (size_t)i * ld + col, src + (size_t)i * cols, (size_t)cols * 4);
+  (void)A;
+  return 0;
+}
+
+static int get_rows(float* dst, int cols, const float* dev, const float* host, int ld, int n, hipStream_t s) {
+  if (host) {
+    for (int i = 0; i < n; ++i) memcpy(dst + (size_t)i * cols, host + (size_t)i * ld, (size_t)cols * 4);
+    return 0;
+  }
+  TD3_HIP(hipMemcpy2DAsync(dst, (size_t)cols * 4, dev, (size_t)ld * 4, (size_t)cols * 4, n, hipMemcpyDeviceToHost, s));
+  TD3_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// A featured query of n <= kGemvRows rows: layers 0 and 1 in one gemv01 launch when layer 0 is
+// narrow (the query rows [x0 | x1] in its arguments), else one gemv launch per layer; then the
+// head over 4 rows.
+static int run_gemv(const ActPlan* A, bool q, int n, const float* x0, int c0, const float* x1, int c1,
+                    hipStream_t s) {
+  const GemvArgs(&gv)[3] = q ? A->gv_q : A->gv_act;
+  const int nprob = q ? 2 : 1;
+  int l = 0;
+  if (A->gemv01) {
+    Gemv01Args g = q ? A->g01_q : A->g01_act;
+    g.l1.B = n;
+    const int K0 = c0 + c1;
+    for (int r = 0; r < n; ++r) {
+      memcpy(g.xq + r * K0, x0 + (size_t)r * c0, (size_t)c0 * 4);
+      if (c1) memcpy(g.xq + r * K0 + c0, x1 + (size_t)r * c1, (size_t)c1 * 4);
+    }
+    TD3_RC(launch_gemv01(g, nprob, s));
+    l = 2;
+  }
+  for (; l < 3; ++l) {
+    GemvArgs a = gv[l];
+    a.B = n;
+    TD3_RC(launch_gemv(a, nprob, s));
+  }
+  HeadArgs head = q ? A->head_q : A->head_act;
+  head.B = n;
+  head.Bp = kGemvRows;
+  return launch_heads(head, nprob, s);
+}
+
 int td3_select_action(td3_handle* h, const float* state, float* action_out, int n) {
   TD3_ARG(h && state && action_out, "null argument");
   TD3_ARG(!h->particles, "particle learner: use td3_select_action_particles");
@@ -2305,13 +2455,17 @@ int td3_select_action(td3_handle* h, const float* state, float* action_out, int 
   ActPlan* A;
   TD3_RC(build_act(h, pad32(n), &A));
   hipStream_t s = h->act_stream;
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
   TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
-  TD3_RC(copy_rows_h2d(A->X_S, pad32(h->sd), 0, state, n, h->sd, s));
-  TD3_RC(run_stages(A->act, s));
-  TD3_HIP(hipMemcpy2DAsync(action_out, (size_t)h->ad * 4, A->X_SP + h->sd, (size_t)pad32(h->sd + h->ad) * 4,
-                           (size_t)h->ad * 4, n, hipMemcpyDeviceToHost, s));
-  TD3_HIP(hipStreamSynchronize(s));
-  return 0;
+  if (A->gemv && n <= kGemvRows) {
+    if (!A->gemv01) TD3_RC(put_rows(A, A->X_S, A->hX_S, pad32(h->sd), 0, state, n, h->sd, s));
+    TD3_RC(run_gemv(A, false, n, state, h->sd, nullptr, 0, s));
+  } else {
+    TD3_RC(put_rows(A, A->X_S, A->hX_S, pad32(h->sd), 0, state, n, h->sd, s));
+    TD3_RC(run_stages(A->act, s));
+  }
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
+  return get_rows(action_out, h->ad, A->out, A->hout, A->ldo, n, s);
 }
 
 int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_out, int n) {
@@ -2323,13 +2477,17 @@ int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_
   TD3_RC(build_act(h, pad32(n), &A));
   hipStream_t s = h->stream;
   const int ld = pad32(h->sd + h->ad);
-  TD3_RC(copy_rows_h2d(A->X_SA, ld, 0, state, n, h->sd, s));
-  TD3_RC(copy_rows_h2d(A->X_SA, ld, h->sd, action, n, h->ad, s));
-  TD3_RC(run_stages(A->evalq, s));
-  TD3_HIP(hipMemcpyAsync(q_out, A->Q[0].Qv, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-  TD3_HIP(hipMemcpyAsync(q_out + n, A->Q[1].Qv, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-  TD3_HIP(hipStreamSynchronize(s));
-  return 0;
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
+  const bool small = A->gemv && n <= kGemvRows;
+  if (!small || !A->gemv01) {
+    TD3_RC(put_rows(A, A->X_SA, A->hX_SA, ld, 0, state, n, h->sd, s));
+    TD3_RC(put_rows(A, A->X_SA, A->hX_SA, ld, h->sd, action, n, h->ad, s));
+  }
+  if (small) TD3_RC(run_gemv(A, true, n, state, h->sd, action, h->ad, s));
+  else TD3_RC(run_stages(A->evalq, s));
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
+  TD3_RC(get_rows(q_out, 1, A->q[0], A->hq[0], 1, n, s));
+  return get_rows(q_out + n, 1, A->q[1], A->hq[1], 1, n, s);
 }
 
 int td3_train_step_batch_particles(td3_handle* h, const float* feat, const float* part, const float* action,
@@ -2382,16 +2540,15 @@ int td3_select_action_particles(td3_handle* h, const float* feat, const float* p
   ActPlan* A;
   TD3_RC(build_act_particles(h, pad32(n), &A));
   hipStream_t s = h->act_stream;
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
   TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
   const int np = h->N * h->D;
   const NetL& an = h->actor.nets[0];
-  TD3_RC(copy_rows_h2d(A->X_S, an.lin[0].Kp, kEncC2, feat, n, h->sd, s));
-  TD3_HIP(hipMemcpyAsync(A->pbatch, part, (size_t)n * np * 4, hipMemcpyHostToDevice, s));
+  TD3_RC(put_rows(A, A->X_S, A->hX_S, an.lin[0].Kp, kEncC2, feat, n, h->sd, s));
+  TD3_RC(put_rows(A, A->pbatch, A->hpbatch, np, 0, part, n, np, s));
   TD3_RC(run_stages(A->act, s));
-  TD3_HIP(hipMemcpy2DAsync(action_out, (size_t)h->ad * 4, A->out, 32 * 4, (size_t)h->ad * 4, n,
-                           hipMemcpyDeviceToHost, s));
-  TD3_HIP(hipStreamSynchronize(s));
-  return 0;
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
+  return get_rows(action_out, h->ad, A->out, A->hout, A->ldo, n, s);
 }
 
 int td3_eval_q_particles(td3_handle* h, const float* feat, const float* part, const float* action, float* q_out,
@@ -2406,17 +2563,20 @@ int td3_eval_q_particles(td3_handle* h, const float* feat, const float* part, co
   const int np = h->N * h->D, F = h->sd, ad = h->ad;
   const int ldq = h->critic.nets[0].lin[0].Kp;
   const bool cdq = h->cdq != 0;
-  for (float* X : {A->X_SA, A->XQ2}) {
-    if (X == A->XQ2 && !cdq) continue;
-    TD3_RC(copy_rows_h2d(X, ldq, kEncC2, feat, n, F, s));
-    TD3_RC(copy_rows_h2d(X, ldq, kEncC2 + F, action, n, ad, s));
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
+  for (int j = 0; j < (cdq ? 2 : 1); ++j) {
+    float* X = j ? A->XQ2 : A->X_SA;
+    float* hX = j ? A->hXQ2 : A->hX_SA;
+    TD3_RC(put_rows(A, X, hX, ldq, kEncC2, feat, n, F, s));
+    TD3_RC(put_rows(A, X, hX, ldq, kEncC2 + F, action, n, ad, s));
   }
-  TD3_HIP(hipMemcpyAsync(A->pbatch, part, (size_t)n * np * 4, hipMemcpyHostToDevice, s));
+  TD3_RC(put_rows(A, A->pbatch, A->hpbatch, np, 0, part, n, np, s));
   TD3_RC(run_stages(A->evalq, s));
-  for (int j = 0; j < 2; ++j)
-    TD3_HIP(hipMemcpy2DAsync(q_out + (size_t)j * n * ad, (size_t)ad * 4, A->Q[cdq ? j : 0].Qv, 32 * 4,
-                             (size_t)ad * 4, n, hipMemcpyDeviceToHost, s));
-  TD3_HIP(hipStreamSynchronize(s));
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
+  for (int j = 0; j < 2; ++j) {
+    const int k = cdq ? j : 0;
+    TD3_RC(get_rows(q_out + (size_t)j * n * ad, ad, A->q[k], A->hq[k], 32, n, s));
+  }
   return 0;
 }
 

@@ -8,9 +8,12 @@ Drop-in for ``/root/reference/my_replay_buffer.py``:
 * ``ReplayBuffer_particles`` (:6-69), the same over (features, particles) states.
 
 The storage lives in HBM (``libtd3hip``'s ring, one fp32 record per transition).
-``add`` stages rows on the host and ships them in batches (pinned memory, async
-H2D); ``sample`` / ``TD3.train`` flush first, so a transition added at step t is
-samplable at step t exactly as in the reference (main.py:261 before :269).
+``add`` writes the transition straight into a host array of ring records (the fp32
+cast the reference makes at ``sample``, :122-127, made once at ``add``: the same
+rounding of the same float64 values) and ``flush`` ships the staged records in one
+``rb_add_records`` call; ``sample`` / ``TD3.train`` flush first, so a transition
+added at step t is samplable at step t exactly as in the reference (main.py:261
+before :269).
 ``sample`` draws indices with a device Philox stream instead of the global numpy
 MT19937 (``np.random.randint`` at :120) -- a documented, deliberate difference.
 """
@@ -39,6 +42,20 @@ def default_device_index() -> int:
     if "LOCAL_RANK" in os.environ:
         return int(os.environ["LOCAL_RANK"]) % torch.cuda.device_count()
     return torch.cuda.current_device()
+
+
+def _new_stage(buf, rows):
+    """Host records staged by ``add`` (zeroed: the record pad stays 0) and their float*."""
+    buf._stage = np.zeros((rows, buf.record_floats), dtype=np.float32)
+    buf._stage_ptr = _lib.fptr(buf._stage)
+    buf._n = 0
+
+
+def _flush_stage(buf):
+    n = buf._n
+    if n:
+        buf._n = 0
+        check(buf._lib.rb_add_records(buf._h, buf._stage_ptr, n, None), "rb_add_records")
 
 
 class _SafeIntUnpickler(pickle.Unpickler):
@@ -91,7 +108,7 @@ class ReplayBuffer_featured(object):
         self.device = torch.device("cuda", self._dev)
         self.seed = int(seed)
         self._h = None
-        self._pending = []
+        self._n = 0
         if load_folder is not None:
             self.load(load_folder)
         else:
@@ -110,6 +127,11 @@ class ReplayBuffer_featured(object):
         self.max_size = max_size
         info = self._info()
         self.record_floats = info.record_floats
+        _new_stage(self, _STAGE_ROWS)
+        sd, ad = self.state_dim, self.action_dim
+        # replay.h record: [ s | a | s' | r | not_done | pad ]
+        self._cols = (slice(0, sd), slice(sd, sd + ad), slice(sd + ad, 2 * sd + ad),
+                      slice(2 * sd + ad, 2 * sd + ad + 1), slice(2 * sd + ad + 1, 2 * sd + ad + 2))
 
     def _info(self):
         info = _lib.rb_info_t()
@@ -138,13 +160,17 @@ class ReplayBuffer_featured(object):
 
     # ------------------------------------------------------------------ reference API
     def add(self, state, action, next_state, reward, done):
-        """my_replay_buffer.py:109-117 (stores not_done = 1 - done)."""
-        self._pending.append((np.asarray(state, dtype=np.float64).reshape(self.state_dim),
-                              np.asarray(action, dtype=np.float64).reshape(self.action_dim),
-                              np.asarray(next_state, dtype=np.float64).reshape(self.state_dim),
-                              float(np.asarray(reward, dtype=np.float64).reshape(-1)[0]),
-                              float(np.asarray(done, dtype=np.float64).reshape(-1)[0])))
-        if len(self._pending) >= _STAGE_ROWS:
+        """my_replay_buffer.py:109-117 (stores not_done = 1 - done): numpy row assignment as the
+        reference's, into the staged fp32 record."""
+        row = self._stage[self._n]
+        cs, ca, cs2, cr, cnd = self._cols
+        row[cs] = state
+        row[ca] = action
+        row[cs2] = next_state
+        row[cr] = reward
+        row[cnd] = 1. - np.asarray(done, dtype=np.float64)
+        self._n += 1
+        if self._n == len(self._stage):
             self.flush()
 
     def add_batch(self, state, action, next_state, reward, done):
@@ -160,17 +186,7 @@ class ReplayBuffer_featured(object):
                                _lib.dptr(d), n, self._stream()), "rb_add")
 
     def flush(self):
-        if not self._pending:
-            return
-        rows = self._pending
-        self._pending = []
-        s = np.stack([x[0] for x in rows])
-        a = np.stack([x[1] for x in rows])
-        s2 = np.stack([x[2] for x in rows])
-        r = np.array([x[3] for x in rows], dtype=np.float64)
-        d = np.array([x[4] for x in rows], dtype=np.float64)
-        check(self._lib.rb_add(self._h, _lib.dptr(s), _lib.dptr(a), _lib.dptr(s2), _lib.dptr(r),
-                               _lib.dptr(d), len(rows), self._stream()), "rb_add")
+        _flush_stage(self)
 
     def fill_synthetic(self, n, max_action=1.0, seed=0):
         """Device-side prefill with the SURVEY §8(d) synthetic distribution (bench/tests)."""
@@ -238,7 +254,7 @@ class ReplayBuffer_featured(object):
 
     def load(self, folder):
         """my_replay_buffer.py:101-107 (pickles are read by an int-only unpickler)."""
-        self._pending = []                  # rows added before a load are replaced with it
+        self._n = 0                         # rows added before a load are replaced with it
         ptr = _load_int(os.path.join(folder, "ptr.pkl"))
         size = _load_int(os.path.join(folder, "size.pkl"))
         arrs = {}
@@ -292,7 +308,7 @@ class ReplayBuffer_particles(object):
         self.device = torch.device("cuda", self._dev)
         self.seed = int(seed)
         self._h = None
-        self._pending = []
+        self._n = 0
         if load_folder is not None:
             self.load(load_folder)
         else:
@@ -310,6 +326,8 @@ class ReplayBuffer_particles(object):
         self._h = h
         self.max_size = max_size
         self.record_floats = self._info().record_floats
+        _new_stage(self, max(1, _STAGE_ROWS // 16))
+        self._cols = tuple(slice(c, c + w) for c, w in self._offsets().values())
 
     def _info(self):
         info = _lib.rb_info_t()
@@ -342,15 +360,18 @@ class ReplayBuffer_particles(object):
     # ------------------------------------------------------------------ reference API
     def add(self, state, action, next_state, reward, done):
         """my_replay_buffer.py:46-56 (state = (features, particles); stores 1 - done)."""
-        F, npd = self.feat_dim, self._np()
-        self._pending.append((np.asarray(state[0], dtype=np.float64).reshape(F),
-                              np.asarray(state[1], dtype=np.float64).reshape(npd),
-                              np.asarray(action, dtype=np.float64).reshape(self.action_dim),
-                              np.asarray(next_state[0], dtype=np.float64).reshape(F),
-                              np.asarray(next_state[1], dtype=np.float64).reshape(npd),
-                              float(np.asarray(reward, dtype=np.float64).reshape(-1)[0]),
-                              float(np.asarray(done, dtype=np.float64).reshape(-1)[0])))
-        if len(self._pending) >= max(1, _STAGE_ROWS // 16):
+        row = self._stage[self._n]
+        cf, cp, ca, cf2, cp2, cr, cnd = self._cols
+        nd = (self.n_particles, self.particle_dim)
+        row[cf] = state[0]
+        row[cp].reshape(nd)[...] = state[1]
+        row[ca] = action
+        row[cf2] = next_state[0]
+        row[cp2].reshape(nd)[...] = next_state[1]
+        row[cr] = reward
+        row[cnd] = 1. - np.asarray(done, dtype=np.float64)
+        self._n += 1
+        if self._n == len(self._stage):
             self.flush()
 
     def add_batch(self, feat, part, action, next_feat, next_part, reward, done):
@@ -368,14 +389,7 @@ class ReplayBuffer_particles(object):
               "rb_add_particles")
 
     def flush(self):
-        if not self._pending:
-            return
-        rows = self._pending
-        self._pending = []
-        cols = [np.stack([r[i] for r in rows]) for i in range(5)]
-        cols += [np.array([r[5] for r in rows], dtype=np.float64), np.array([r[6] for r in rows], dtype=np.float64)]
-        check(self._lib.rb_add_particles(self._h, *[_lib.dptr(np.ascontiguousarray(x)) for x in cols],
-                                         len(rows), self._stream()), "rb_add_particles")
+        _flush_stage(self)
 
     def fill_synthetic(self, n, max_action=1.0, seed=0):
         self.flush()
@@ -442,7 +456,7 @@ class ReplayBuffer_particles(object):
 
     def load(self, folder):
         """my_replay_buffer.py:34-44 (int-only unpickler for ptr / size)."""
-        self._pending = []                  # rows added before a load are replaced with it
+        self._n = 0                         # rows added before a load are replaced with it
         ptr = _load_int(os.path.join(folder, "ptr.pkl"))
         size = _load_int(os.path.join(folder, "size.pkl"))
         arrs = {}

@@ -185,6 +185,31 @@ def test_select_action_and_eval_q():
         np.testing.assert_allclose(q[1], q2[0], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("name", ["hc_layer", "hc_none"])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 300])
+def test_select_action_eval_q_batch_paths(name, n):
+    """The query paths of td3.hip: n <= 4 rows on the gemv chain (gemv_kernel<1, 2, 4>), up to 256
+    padded rows on the GEMM stages with mapped host I/O, more on device buffers and DMA copies
+    (kMappedRows) -- actions and both Q values against the oracle row by row; two calls in a
+    row reuse the plan's buffers."""
+    from td3_amd import _lib
+    S = featured_setup(name)
+    pol, _ = _make(S)
+    rs = np.random.RandomState(n)
+    for _ in range(2):
+        st = rs.standard_normal((n, S["sd"])).astype(np.float32)
+        got = pol.select_action_batch(st)
+        assert got.shape == (n, S["ad"])
+        q = np.empty(2 * n, np.float32)
+        _lib.check(pol._lib.td3_eval_q(pol._h, _lib.fptr(st), _lib.fptr(got), _lib.fptr(q), n), "td3_eval_q")
+        q1, _ = orc.featured_q(S["critic"], "q1", S["norm"], st, got)
+        q2, _ = orc.featured_q(S["critic"], "q2", S["norm"], st, got)
+        assert _rel_to_max(q[:n], q1[:, 0]) <= 1e-5
+        assert _rel_to_max(q[n:], q2[:, 0]) <= 1e-5
+        ref = np.stack([orc.featured_select_action(S["actor"], S["norm"], S["ma"], st[i]) for i in range(n)])
+        assert _rel_to_max(got, ref) <= 1e-5
+
+
 def test_foreign_buffer_path():
     """A duck-typed buffer (the reference's own class shape) goes through sample() tensors."""
     S = featured_setup("hc_layer")
