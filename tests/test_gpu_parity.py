@@ -210,6 +210,24 @@ def test_select_action_eval_q_batch_paths(name, n):
         assert _rel_to_max(got, ref) <= 1e-5
 
 
+@pytest.mark.parametrize("n", [1, 4, 40])
+def test_select_action_eval_q_wide_input(n):
+    """Humanoid widths (sd 376, ad 17): a layer 0 wider than gemv01 takes (kGemv0K = 64), so
+    n <= 4 runs one gemv launch per layer reading the query from mapped host memory."""
+    from td3_amd import _lib
+    S = featured_setup_dims(376, 17, ma=0.4)
+    pol, _ = _make(S)
+    st = np.random.RandomState(n).standard_normal((n, 376)).astype(np.float32)
+    got = pol.select_action_batch(st)
+    ref = np.stack([orc.featured_select_action(S["actor"], S["norm"], S["ma"], x) for x in st])
+    assert _rel_to_max(got, ref) <= 1e-5
+    q = np.empty(2 * n, np.float32)
+    _lib.check(pol._lib.td3_eval_q(pol._h, _lib.fptr(st), _lib.fptr(got), _lib.fptr(q), n), "td3_eval_q")
+    for j, qn in enumerate(("q1", "q2")):
+        qr, _ = orc.featured_q(S["critic"], qn, S["norm"], st, got)
+        assert _rel_to_max(q[j * n:(j + 1) * n], qr[:, 0]) <= 1e-5
+
+
 def test_foreign_buffer_path():
     """A duck-typed buffer (the reference's own class shape) goes through sample() tensors."""
     S = featured_setup("hc_layer")

@@ -139,6 +139,22 @@ def test_particle_select_action_and_eval_q():
             np.testing.assert_allclose(q[j], qr[0], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("n", [3, 40])
+def test_particle_select_action_batch(n):
+    """Several particle queries in one call (mapped host I/O up to 256 padded rows)."""
+    from td3_amd import _lib
+    S = particle_setup("part_layer")
+    pol, _ = _make(S)
+    rs = np.random.RandomState(n)
+    f = rs.standard_normal((n, S["F"])).astype(np.float32)
+    p = rs.standard_normal((n, S["N"], S["D"])).astype(np.float32)
+    out = np.empty((n, S["A"]), np.float32)
+    _lib.check(pol._lib.td3_select_action_particles(pol._h, _lib.fptr(f), _lib.fptr(p), _lib.fptr(out), n),
+               "td3_select_action_particles")
+    ref, _ = orc.particle_net(S["actor"], "", S["norm"], f, p, actor=True)
+    assert float(np.abs(out - ref).max()) <= 1e-5 * float(np.abs(ref).max()) + 1e-6
+
+
 def test_particle_foreign_buffer_path():
     S = particle_setup("part_nocdq")
     G = load_golden("particles", "part_nocdq")
