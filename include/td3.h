@@ -97,7 +97,7 @@ typedef struct td3_config {
   int state_dim, action_dim;
   int actor_hidden[3];     /* reference: (500, 400, 300)  TD3_featured.py:19 */
   int critic_hidden[3];    /* reference: (500, 400, 200)  TD3_featured.py:54 */
-  int norm;                /* 0: None, 1: "layer"  (TD3_featured.py:28-31) */
+  int norm;                /* 0: None, 1: "layer" (TD3_featured.py:28-31), 2: "weight_normalization" (:33-35, 68-70; featured only) */
   float max_action;
   double discount, tau, policy_noise, noise_clip;   /* TD3_base.py:9-13 */
   int policy_freq;

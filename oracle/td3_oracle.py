@@ -21,6 +21,9 @@ Reference functions restated here (``/root/reference/...``):
 * ``TD3_particles.py:52-69,103-119`` encoder + MLP -> ``encoder_forward`` / ``particle_*``
 * ``TD3_particles.py:167-224``     TD3.train / _actor_learn -> ``particle_train_step``
 * torch 2.10 ``_single_tensor_adam`` (torch/optim/adam.py:347, math :457-547) -> ``adam_``
+* ``TD3_featured.py:33-35, 68-70`` norm="weight_normalization": torch ``weight_norm`` (dim 0)
+  on every Linear, W = v * (g / ||v||) per output row, dg = (dW . v)/||v||,
+  dv = (g/||v||) dW - (g (dW . v)/||v||^3) v  -> ``wn_weight`` / ``wn_grads``
 """
 from __future__ import annotations
 
@@ -31,8 +34,27 @@ LN_EPS = f32(1e-5)
 
 
 # --------------------------------------------------------------------------- params
+def wn_weight(g, v):
+    """torch ``_weight_norm_interface`` (dim 0): W = v * (g / ||v||), ||v|| per output row."""
+    n = np.sqrt((v.astype(np.float64) ** 2).sum(axis=1, keepdims=True)).astype(f32)
+    return (v * (g / n)).astype(f32)
+
+
+def wn_grads(gW, g, v):
+    """Backward of ``wn_weight``: (dL/dg [N,1], dL/dv [N,K]) from dL/dW."""
+    n = np.sqrt((v.astype(np.float64) ** 2).sum(axis=1, keepdims=True)).astype(f32)
+    s = (gW.astype(np.float64) * v).sum(axis=1, keepdims=True).astype(f32)
+    a = (g / n).astype(f32)
+    b = (a * s / (n * n)).astype(f32)
+    return (s / n).astype(f32), (a * gW - b * v).astype(f32)
+
+
 def split_mlp(P, prefix, n_layers, norm, first_norm=False):
     """Collect (W, b) per Linear and (gamma, beta) per LayerNorm from a state dict."""
+    if norm == "weight_normalization":
+        lin = [(wn_weight(P[f"{prefix}linears.{i}.weight_g"], P[f"{prefix}linears.{i}.weight_v"]),
+                P[f"{prefix}linears.{i}.bias"]) for i in range(n_layers)]
+        return lin, None, None
     lin = [(P[f"{prefix}linears.{i}.weight"], P[f"{prefix}linears.{i}.bias"]) for i in range(n_layers)]
     ln = None
     ln0 = None
@@ -122,10 +144,17 @@ def mlp_backward(lin, ln, cache, gz_last):
     raise AssertionError("unreachable")
 
 
-def pack_mlp_grads(prefix, grads, norm, extra=None):
+def pack_mlp_grads(prefix, grads, norm, extra=None, P=None):
+    """Gradients in state-dict order; weight_normalization maps dW to (weight_g, weight_v)
+    through the parameters ``P`` the backward ran with."""
     gW, gb, gg, gbeta = grads
     out = {}
     for i in range(len(gW)):
+        if norm == "weight_normalization":
+            out[f"{prefix}linears.{i}.bias"] = gb[i]
+            out[f"{prefix}linears.{i}.weight_g"], out[f"{prefix}linears.{i}.weight_v"] = wn_grads(
+                gW[i], P[f"{prefix}linears.{i}.weight_g"], P[f"{prefix}linears.{i}.weight_v"])
+            continue
         out[f"{prefix}linears.{i}.weight"] = gW[i]
         out[f"{prefix}linears.{i}.bias"] = gb[i]
     if extra:
@@ -301,7 +330,7 @@ def featured_train_step(L: Learner, batch, noise, record=None, grad_hook=None):
     for q, qv, (lin, ln, cache) in (("q1", q1, c1), ("q2", q2, c2)):
         gq = (f32(2.0 / (B)) * (qv - y)).astype(f32)                          # d mse / dQ
         g, _ = mlp_backward(lin, ln, cache, gq)
-        grads.update(pack_mlp_grads(f"{q}.", g, L.norm))
+        grads.update(pack_mlp_grads(f"{q}.", g, L.norm, P=L.critic))
     rec["critic_grads"] = grads
     L.adam_critic(hook(grads))                                                 # :151-153
     if L.total_it % L.policy_freq == 0:                                        # :156
@@ -313,7 +342,7 @@ def featured_train_step(L: Learner, batch, noise, record=None, grad_hook=None):
         gpi = gx[:, s.shape[1]:]
         gz = (gpi * f32(L.max_action)) * (f32(1) - t * t)                       # tanh'
         ag, _ = mlp_backward(alin, aln, acache, gz.astype(f32))
-        agrads = pack_mlp_grads("", ag, L.norm)
+        agrads = pack_mlp_grads("", ag, L.norm, P=L.actor)
         rec["actor_grads"] = agrads
         L.adam_actor(hook(agrads))                                             # :162-164
         L.polyak()                                                             # :167-171

@@ -166,6 +166,16 @@ def torch_default_init(sd, ad, norm, actor_arch=ACTOR_ARCH, q_arch=Q_ARCH):
         lin = [nn.Linear(dims[i], dims[i + 1]) for i in range(len(arch))] + [nn.Linear(arch[-1], out)]
         d = OrderedDict()
         for i, l in enumerate(lin):
+            if norm == "weight_normalization":
+                # torch.nn.utils.weight_norm(Linear) (TD3_featured.py:33-35, 68-70, dim 0): v = W,
+                # g = ||W|| per output row; it draws no random numbers
+                import warnings
+                with warnings.catch_warnings():
+                    warnings.simplefilter("ignore", FutureWarning)
+                    l = nn.utils.weight_norm(l)
+                for k in ("bias", "weight_g", "weight_v"):
+                    d[f"{prefix}linears.{i}.{k}"] = getattr(l, k).detach().numpy().copy()
+                continue
             d[f"{prefix}linears.{i}.weight"] = l.weight.detach().numpy().copy()
             d[f"{prefix}linears.{i}.bias"] = l.bias.detach().numpy().copy()
         if norm == "layer":
@@ -188,9 +198,8 @@ class TD3(TD3_base):
                  init="torch", **kwargs):
         super().__init__(max_action=max_action, **kwargs)
         self._lib = _lib.load()
-        if norm not in (None, "layer"):
-            raise ValueError(f"norm={norm!r} is not supported (None or 'layer'; the reference's "
-                             "'weight_normalization' crashes on deepcopy, SURVEY.md F8)")
+        if norm not in (None, "layer", "weight_normalization"):
+            raise ValueError(f"norm={norm!r} is not supported (None, 'layer' or 'weight_normalization')")
         self.norm = norm
         self.CDQ = CDQ          # TD3_featured ignores it (always twin critics), :100
         sd, ad = int(obs_space.shape[0]), int(action_space.shape[0])
@@ -204,7 +213,7 @@ class TD3(TD3_base):
         for i in range(3):
             cfg.actor_hidden[i] = actor_arch[i]
             cfg.critic_hidden[i] = q_arch[i]
-        cfg.norm = 1 if norm == "layer" else 0
+        cfg.norm = {None: 0, "layer": 1, "weight_normalization": 2}[norm]
         cfg.max_action = float(max_action)
         cfg.discount, cfg.tau = float(self.discount), float(self.tau)
         cfg.policy_noise, cfg.noise_clip = float(self.policy_noise), float(self.noise_clip)

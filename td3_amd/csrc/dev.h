@@ -311,7 +311,8 @@ __device__ __forceinline__ AdamK make_adam(const AdamArgs& a, const AdamPw& pw) 
 __device__ __forceinline__ AdamK make_adam(const AdamArgs& a) { return make_adam(a, adam_pw(a)); }
 
 // torch _single_tensor_adam (adam.py:520-547): lerp, mul/addcmul, sqrt/div/add, addcdiv.
-__device__ __forceinline__ void adam_elem(float* __restrict__ p, float* __restrict__ m,
+// Returns the updated (parameter, target); the target is 0 without Polyak.
+__device__ __forceinline__ float2 adam_elem(float* __restrict__ p, float* __restrict__ m,
                                           float* __restrict__ v, float g, const AdamK& k,
                                           float* __restrict__ t) {
   float mm = gld(m), vv = gld(v), pp = gld(p);
@@ -323,7 +324,12 @@ __device__ __forceinline__ void adam_elem(float* __restrict__ p, float* __restri
   gst(m, mm);
   gst(v, vv);
   gst(p, pp);
-  if (t) gst(t, k.tau * pp + k.omt * gld(t));     // TD3_featured.py:167-171
+  float tt = 0.f;
+  if (t) {
+    tt = k.tau * pp + k.omt * gld(t);              // TD3_featured.py:167-171
+    gst(t, tt);
+  }
+  return make_float2(pp, tt);
 }
 
 }  // namespace td3

@@ -220,6 +220,27 @@ int launch_heads(const HeadArgs& a, int nprob, hipStream_t s);
 int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s);
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s);
 int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s);
+
+// ------------------------------------------------------------------ weight normalization
+// norm = "weight_normalization" (TD3_featured.py:33-35, 68-70: torch weight_norm, dim 0, on
+// every Linear): the parameters of a Linear are bias, weight_g [N,1] and weight_v [N,K]; the
+// GEMM stages read the derived W = v * (g / ||v||) kept at the Linear's weight offset.
+struct WnLinear {
+  int64_t offW, offb, offg, offv;    // offsets in a group arena (W and v: [Np][Kp] rows)
+  int N, K, ld;                      // real rows / columns, row stride Kp
+  int row0;                          // first row of this Linear in the launch's row numbering
+};
+constexpr int kMaxWnLinears = 8;     // 4 Linears x 2 networks (twin critic)
+struct WnArgs {
+  WnLinear lin[kMaxWnLinears];
+  int nlin, rows;                    // rows = sum of N: one wave per output row
+  AdamArgs adam;                     // P, T, M, V, G arenas, counters, hyper-parameters
+  int mode;                          // kWnDerive: W of `arena` (and `arena2`); kWnAdam: optimizer step
+  int polyak;                        // kWnAdam: Polyak the targets (T) too and re-derive their W
+  float* arena; float* arena2;       // kWnDerive
+};
+enum WnMode : int { kWnDerive = 0, kWnAdam = 1 };
+int launch_wn(const WnArgs& a, hipStream_t s);
 int launch_polyak_flat(float* T, const float* P, int64_t n, float tau, hipStream_t s);
 int kernels_init();
 

@@ -2087,6 +2087,89 @@ __global__ __launch_bounds__(256) void polyak_flat_kernel(float* T, const float*
     gst(T + i, tau * gld(P + i) + omt * gld(T + i));
 }
 
+// ================================================================== weight normalization
+// One wave per output row of a weight-normalised Linear (K <= 512: 8 columns per lane).
+// kWnAdam: the row's dL/dW (G arena, dw_kernel in kDwGrad mode, all-reduced when data
+// parallel) becomes torch's weight_norm backward
+//   dg = (dW . v) / ||v||,   dv = (g / ||v||) dW - (g (dW . v) / ||v||^3) v
+// then Adam on (bias, g, v) with the group's moments (adam_elem, + Polyak of the targets) and
+// the row of W = v * (g / ||v||) is derived again from the updated parameters (and targets).
+__device__ __forceinline__ float wn_norm(const float (&v)[8], int K, int lane) {
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (rcol(lane, j) < K) q += v[j] * v[j];
+  return sqrtf(wsum(q));
+}
+
+__device__ __forceinline__ void wn_store_w(float* arena, const WnLinear& L, int i, int lane, float (&v)[8],
+                                           float g) {
+  const float sc = g / wn_norm(v, L.K, lane);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = v[j] * sc;
+  rv_store(arena + L.offW + (size_t)i * L.ld, L.K, lane, v);
+}
+
+__device__ __forceinline__ float lane0(float x) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+}
+
+__global__ __launch_bounds__(256) void wn_kernel(WnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  int l = 0;
+  while (l + 1 < a.nlin && r >= a.lin[l + 1].row0) ++l;
+  const WnLinear& L = a.lin[l];
+  const int i = r - L.row0;
+  float v[8];
+  if (a.mode == kWnDerive) {
+    for (float* arena : {a.arena, a.arena2}) {
+      if (!arena) continue;
+      rv_load(v, arena + L.offv + (size_t)i * L.ld, L.K, lane);
+      wn_store_w(arena, L, i, lane, v, gld(arena + L.offg + i));
+    }
+    return;
+  }
+  const AdamArgs& A = a.adam;
+  const AdamK k = make_adam(A);
+  float gw[8], vt[8];
+  rv_load(v, A.P + L.offv + (size_t)i * L.ld, L.K, lane);
+  rv_load(gw, A.G + L.offW + (size_t)i * L.ld, L.K, lane);
+  const float g = gld(A.P + L.offg + i);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gw[j] *= k.gscale;
+  const float n = wn_norm(v, L.K, lane);
+  const float sdot = wsum(rv_pdot(gw, v, L.K, lane));
+  const float ca = g / n;
+  const float cb = ca * sdot / (n * n);
+  const float dg = sdot / n;
+  float* T = a.polyak ? A.T : nullptr;
+  // v: the lane's 8 columns, element-wise Adam; the updated values stay in registers
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = rcol(lane, j);
+    vt[j] = 0.f;
+    if (c < L.K) {
+      const size_t o = L.offv + (size_t)i * L.ld + c;
+      const float2 u = adam_elem(A.P + o, A.M + o, A.V + o, ca * gw[j] - cb * v[j], k, T ? T + o : nullptr);
+      v[j] = u.x;
+      vt[j] = u.y;
+    } else {
+      v[j] = 0.f;
+    }
+  }
+  float2 ug = make_float2(0.f, 0.f);
+  if (lane == 0) {
+    const size_t og = L.offg + i, ob = L.offb + i;
+    ug = adam_elem(A.P + og, A.M + og, A.V + og, dg, k, T ? T + og : nullptr);
+    (void)adam_elem(A.P + ob, A.M + ob, A.V + ob, gld(A.G + ob) * k.gscale, k, T ? T + ob : nullptr);
+  }
+  const float gn = lane0(ug.x), gt = lane0(ug.y);
+  wn_store_w(A.P, L, i, lane, v, gn);
+  if (T) wn_store_w(T, L, i, lane, vt, gt);
+}
+
 // ================================================================== launchers
 template <int MODE, int WN, int PRO>
 static void gl(const GemmTable& t, int nblocks, int Bp, int lds, Counters* bump, int ba, hipStream_t s) {
@@ -2323,6 +2406,21 @@ int launch_dw(const DwArgs& a, int nblocks, hipStream_t s) {
 int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s) {
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, a, n, polyak);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_wn(const WnArgs& a, hipStream_t s) {
+  if (a.nlin < 1 || a.nlin > kMaxWnLinears || a.rows < 1) {
+    set_error("launch_wn: %d linears (max %d), %d rows", a.nlin, kMaxWnLinears, a.rows);
+    return -1;
+  }
+  for (int l = 0; l < a.nlin; ++l)
+    if (a.lin[l].K < 1 || a.lin[l].K > 512) {
+      set_error("launch_wn: input width %d (max 512)", a.lin[l].K);
+      return -1;
+    }
+  hipLaunchKernelGGL(wn_kernel, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
   TD3_HIP(hipGetLastError());
   return 0;
 }

@@ -43,7 +43,9 @@ void set_error(const char* fmt, ...) {
 }
 
 // ------------------------------------------------------------------ layouts
-struct LinearL { int N, K, Np, Kp; int64_t offW, offb; };
+// offW: the weight the GEMM stages read; with weight normalization it is derived from
+// (offg, offv) = (weight_g [Np], weight_v [Np][Kp]) by wn_kernel, else offg = offv = -1.
+struct LinearL { int N, K, Np, Kp; int64_t offW, offb, offg = -1, offv = -1; };
 struct LNormL { int N, Np; int64_t offg, offb; };
 struct NetL {
   LinearL lin[4];
@@ -62,14 +64,18 @@ struct Group {
   float *P = nullptr, *T = nullptr, *M = nullptr, *V = nullptr, *G = nullptr;
   std::vector<NetL> nets;
   std::vector<TensorRef> tensors;
+  WnArgs wn{};               // weight normalization: the group's Linears (wn.nlin = 0 otherwise)
 };
 
 // Parameter layout of one network in reference state_dict order.  Featured (TD3_featured.py:
-// 15-37 / 50-71): linears.{0..3}, lnorms.{0..2}.  Particles (TD3_particles.py:19-50 / 71-101):
-// conv1, conv2, linears.{0..3}, lnorm1, lnorms.{0..2}.
-static NetL layout_mlp(int in, const int hid[3], int out, bool norm, const std::string& prefix,
+// 15-37 / 50-71): linears.{0..3}, lnorms.{0..2}; with weight normalization (:33-35, 68-70)
+// linears.{i}.{bias, weight_g, weight_v} (torch weight_norm's registration order) and no
+// lnorms.  Particles (TD3_particles.py:19-50 / 71-101): conv1, conv2, linears.{0..3}, lnorm1,
+// lnorms.{0..2}.  norm_kind: 0 None, 1 "layer", 2 "weight_normalization".
+static NetL layout_mlp(int in, const int hid[3], int out, int norm_kind, const std::string& prefix,
                        int64_t& off, std::vector<TensorRef>& tensors, int enc_D = 0) {
   NetL n{};
+  const bool norm = norm_kind == 1, wn = norm_kind == 2;
   if (enc_D > 0) {
     off = (off + 3) & ~(int64_t)3;           // float4 loads of the conv2 weight
     n.D = enc_D;
@@ -92,8 +98,19 @@ static NetL layout_mlp(int in, const int hid[3], int out, bool norm, const std::
     off += (int64_t)L.Np * L.Kp;
     L.offb = off;
     off += L.Np;
-    tensors.push_back({prefix + "linears." + std::to_string(l) + ".weight", L.N, L.K, L.offW, L.Kp});
-    tensors.push_back({prefix + "linears." + std::to_string(l) + ".bias", L.N, 0, L.offb, 0});
+    const std::string name = prefix + "linears." + std::to_string(l);
+    if (wn) {
+      L.offg = off;
+      off += L.Np;
+      L.offv = off;
+      off += (int64_t)L.Np * L.Kp;
+      tensors.push_back({name + ".bias", L.N, 0, L.offb, 0});
+      tensors.push_back({name + ".weight_g", L.N, 1, L.offg, 1});
+      tensors.push_back({name + ".weight_v", L.N, L.K, L.offv, L.Kp});
+      continue;
+    }
+    tensors.push_back({name + ".weight", L.N, L.K, L.offW, L.Kp});
+    tensors.push_back({name + ".bias", L.N, 0, L.offb, 0});
   }
   if (enc_D > 0) {
     n.lnin = norm;
@@ -497,7 +514,7 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
                           const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
                           Counters* bump, int bump_actor, const RingSide* ring = nullptr,
                           const RingOut* ro = nullptr, int o_r = 0, bool fuse_l0 = false) {
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   fuse_l0 = fuse_l0 && can_fuse_l0(items);
   for (int l = fuse_l0 ? 1 : 0; l < 3; ++l) {
     std::vector<GemmProb> probs;
@@ -617,7 +634,7 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
                           const std::vector<BwdItem>& items, int Bp, int B, const char* tag,
                           bool need_dz0, bool need_in = false,
                           std::vector<GemmProb>* lnbwd_rows = nullptr) {
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   for (int l = 2; l >= (need_in ? 0 : 1); --l) {
     std::vector<GemmProb> probs;
     int blocks = 0, lds = 0;
@@ -720,7 +737,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                         Group& g, int which, const std::vector<BwdItem>& items, int Bp,
                         const char* tag, bool polyak, int enc_nwg = 0,
                         const std::vector<const float*>* unit_scale = nullptr) {
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   // B >= 512: 64x64 weight tiles with LDS-staged operands (dw64_kernel: half the operand
   // traffic, Humanoid C_dw 73 -> 63 us), else 32x32 register tiles (dw_kernel: more, shorter
   // workgroups for the latency-bound small batches)
@@ -802,7 +819,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.adam.tau = (float)h->cfg.tau;
   a.adam.grad_scale = 1.0f;
   const bool dp = h->comm != nullptr;
-  a.mode = dp ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
+  const bool wn = g.wn.nlin > 0;            // weight normalization: dW -> (dg, dv) in wn_kernel
+  a.mode = (dp || wn) ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
   a.tile64 = tile64 ? 1 : 0;
   a.scaled = unit_scale ? 1 : 0;
   st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
@@ -837,9 +855,18 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                     return 0;
                   },
                   0, "rccl"});
-    AdamArgs aa = a.adam;
-    aa.grad_scale = 1.0f / (float)h->nranks;
-    const int pol = polyak ? 1 : 0;
+  }
+  AdamArgs aa = a.adam;
+  if (dp) aa.grad_scale = 1.0f / (float)h->nranks;
+  const int pol = polyak ? 1 : 0;
+  if (wn) {
+    WnArgs w = g.wn;
+    w.adam = aa;
+    w.mode = kWnAdam;
+    w.polyak = pol;
+    st.push_back({std::string(tag) + "_wn", [=](hipStream_t s) { return launch_wn(w, s); }, 0, "td3::wn_kernel"});
+  } else if (dp) {
+    const int64_t n = g.size;
     st.push_back({std::string(tag) + "_adam",
                   [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s); }, 0,
                   "td3::adam_flat_kernel"});
@@ -890,7 +917,7 @@ static int build_step(td3_handle* h, int B) {
   const int Bp = pad32(B);
   P->B = B;
   P->Bp = Bp;
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   const int sd = h->sd, ad = h->ad;
   P->ld_s = pad32(sd);
   P->ld_sa = pad32(sd + ad);
@@ -1253,7 +1280,7 @@ static int enc_bwd_nwg(int B, int nnets) { return std::max(1, std::min(B, 256 / 
 static void push_enc_bwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const std::vector<BwdItem>& items,
                          const std::vector<float*>& X, const std::string& name) {
   const int N = h->N, D = h->D;
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   const double flops = 2.0 * P->B * N * (2.0 * kEncC2 * kEncC1 + (double)kEncC1 * D) * items.size();
   st.push_back({name,
                 [=](hipStream_t s) {
@@ -1320,7 +1347,7 @@ static int build_step_particles(td3_handle* h, int B) {
   P->B = B;
   P->Bp = Bp;
   P->particles = 1;
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   const bool cdq = h->cdq != 0;
   const int F = h->sd, ad = h->ad, N = h->N, D = h->D;
   const int nqn = cdq ? 2 : 1;
@@ -1808,7 +1835,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
   }
   std::unique_ptr<ActPlan> A(new ActPlan());
   A->Bp = Bp;
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   const NetL& an = h->actor.nets[0];
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[1];
@@ -1935,7 +1962,7 @@ static int build_act_particles(td3_handle* h, int Bp, ActPlan** out) {
   }
   std::unique_ptr<ActPlan> A(new ActPlan());
   A->Bp = Bp;
-  const bool norm = h->cfg.norm != 0;
+  const bool norm = h->cfg.norm == 1;
   const bool cdq = h->cdq != 0;
   const int N = h->N, D = h->D, ad = h->ad;
   const NetL& an = h->actor.nets[0];
@@ -2101,6 +2128,8 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_ARG(cfg->state_dim > 0 && cfg->action_dim > 0, "dims must be positive");
   TD3_ARG(cfg->action_dim <= 32, "action_dim > 32 not supported by the head kernels");
   TD3_ARG(cfg->policy_freq > 0, "policy_freq must be positive");
+  TD3_ARG(cfg->norm >= 0 && cfg->norm <= 2, "norm must be 0 (None), 1 (layer) or 2 (weight_normalization)");
+  TD3_ARG(!(cfg->particles && cfg->norm == 2), "weight_normalization is a TD3_featured option");
   const int in_extra = cfg->particles ? kEncC2 : 0;
   TD3_ARG(pad32(in_extra + cfg->state_dim + cfg->action_dim) <= 512, "network input width must be <= 512");
   if (cfg->particles) {
@@ -2119,7 +2148,7 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   h->adam[0] = h->adam[1] = td3_handle::AdamHp{cfg->lr, cfg->beta1, cfg->beta2, cfg->eps};
   h->sd = cfg->state_dim;
   h->ad = cfg->action_dim;
-  const bool norm = cfg->norm != 0;
+  const int norm = cfg->norm;
   int64_t off = 0;
   if (cfg->particles) {                     // TD3_particles.py:19-50 (Actor), :71-128 (Critic)
     h->particles = 1;
@@ -2170,6 +2199,17 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   {
     const Counters c0 = make_counters(h, 0, 0, 0);
     TD3_HIP(hipMemcpy(h->d_ctr, &c0, sizeof(c0), hipMemcpyHostToDevice));
+  }
+  if (norm == 2) {
+    for (Group* g : {&h->actor, &h->critic}) {
+      WnArgs& w = g->wn;
+      for (const NetL& n : g->nets)
+        for (const LinearL& L : n.lin) {
+          TD3_ARG(w.nlin < kMaxWnLinears, "too many weight-normalised Linears");
+          w.lin[w.nlin++] = WnLinear{L.offW, L.offb, L.offg, L.offv, L.N, L.K, L.Kp, w.rows};
+          w.rows += L.N;
+        }
+    }
   }
   TD3_HIP(hipDeviceSynchronize());          // null-stream memsets vs the handle's non-blocking streams
   TD3_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
@@ -2289,6 +2329,14 @@ int td3_set_params(td3_handle* h, int which, const float* in, int64_t n) {
     }
   }
   TD3_HIP(hipMemcpy(base, host.data(), g->size * 4, hipMemcpyHostToDevice));
+  if (g->wn.nlin > 0 && (base == g->P || base == g->T)) {   // W = v * (g / ||v||) of the new (g, v)
+    WnArgs w = g->wn;
+    w.mode = kWnDerive;
+    w.arena = base;
+    w.arena2 = nullptr;
+    TD3_RC(launch_wn(w, h->stream));
+    TD3_HIP(hipStreamSynchronize(h->stream));
+  }
   return 0;
 }
 

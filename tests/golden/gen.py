@@ -13,6 +13,9 @@ small documented generator instead and *load* the result into the reference
 * Linear / Conv bias     ~ U(-1/sqrt(fan_in), +1/sqrt(fan_in))   (fan_in of its weight)
 * LayerNorm weight       ~ U(0.8, 1.2)      (randomised so the LN affine path is exercised)
 * LayerNorm bias         ~ U(-0.1, 0.1)
+* weight_norm ``weight_v`` as a Linear weight, ``weight_g`` ~ U(0.5, 1.5)  (norm =
+  "weight_normalization": ``torch.nn.utils.weight_norm`` on every Linear, dim 0,
+  TD3_featured.py:33-35 / 68-70; state-dict order bias, weight_g, weight_v)
 
 drawn in ``state_dict`` order from ``numpy.random.RandomState(seed)`` and cast
 to float32.  Replay contents are drawn from ``RandomState(seed + 1)``.
@@ -29,12 +32,15 @@ NUM_FEATURES = 128                # TD3_particles.py:27
 
 def _mlp_shapes(prefix, in_dim, arch, out_dim, norm, first_norm_dim=None):
     shapes = []
-    dims = [in_dim] + list(arch)
-    for i, d in enumerate(arch):
-        shapes.append((f"{prefix}linears.{i}.weight", (d, dims[i])))
-        shapes.append((f"{prefix}linears.{i}.bias", (d,)))
-    shapes.append((f"{prefix}linears.{len(arch)}.weight", (out_dim, arch[-1])))
-    shapes.append((f"{prefix}linears.{len(arch)}.bias", (out_dim,)))
+    dims = [in_dim] + list(arch) + [out_dim]
+    for i in range(len(arch) + 1):
+        if norm == "weight_normalization":
+            shapes.append((f"{prefix}linears.{i}.bias", (dims[i + 1],)))
+            shapes.append((f"{prefix}linears.{i}.weight_g", (dims[i + 1], 1)))
+            shapes.append((f"{prefix}linears.{i}.weight_v", (dims[i + 1], dims[i])))
+        else:
+            shapes.append((f"{prefix}linears.{i}.weight", (dims[i + 1], dims[i])))
+            shapes.append((f"{prefix}linears.{i}.bias", (dims[i + 1],)))
     if norm == "layer":
         if first_norm_dim is not None:
             shapes.append((f"{prefix}lnorm1.weight", (first_norm_dim,)))
@@ -87,18 +93,19 @@ def init_params(shapes, seed):
     """Draw every tensor of ``shapes`` (state-dict order) from RandomState(seed)."""
     rs = np.random.RandomState(seed)
     out = {}
-    fan_in = None
+    # fan_in of every module's weight, so a bias listed before its weight (weight_norm) gets it too
+    fan = {name.rsplit(".", 1)[0]: int(np.prod(shape[1:])) for name, shape in shapes
+           if name.endswith(".weight") or name.endswith(".weight_v")}
     for name, shape in shapes:
+        fan_in = fan.get(name.rsplit(".", 1)[0])
         if "lnorm" in name:
             if name.endswith("weight"):
                 v = rs.uniform(0.8, 1.2, size=shape)
             else:
                 v = rs.uniform(-0.1, 0.1, size=shape)
-        elif name.endswith("weight"):
-            fan_in = int(np.prod(shape[1:]))
-            bound = 1.0 / np.sqrt(fan_in)
-            v = rs.uniform(-bound, bound, size=shape)
-        else:
+        elif name.endswith("weight_g"):
+            v = rs.uniform(0.5, 1.5, size=shape)
+        else:                                       # weight, weight_v, bias
             bound = 1.0 / np.sqrt(fan_in)
             v = rs.uniform(-bound, bound, size=shape)
         out[name] = v.astype(np.float32)
@@ -154,6 +161,7 @@ FEATURED_CONFIGS = {
                     dict(discount=0.999, tau=0.01, lr=3e-4, policy_freq=3,
                          policy_noise=0.3, noise_clip=0.4)),
     "hum_layer": (376, 17, 0.4, "layer", 128, 2, {}),
+    "hc_wn": (17, 6, 1.0, "weight_normalization", 256, 4, {}),
 }
 
 PARTICLE_CONFIGS = {

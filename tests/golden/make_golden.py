@@ -125,10 +125,40 @@ def _load(module, params):
     module.load_state_dict(sd, strict=True)
 
 
+@contextlib.contextmanager
+def _weight_norm_deepcopy(TD3_featured):
+    """``TD3.__init__`` deep-copies the online networks into the targets (TD3_featured.py:102,
+    107).  With ``norm="weight_normalization"`` this torch refuses: ``weight_norm`` keeps the
+    hook-computed ``weight`` as a plain (non-leaf) tensor attribute, and deepcopy only copies
+    graph leaves.  For the duration of the constructor the module's ``copy`` is replaced by one
+    whose deepcopy leaves that attribute out; the copy's forward pre-hook recomputes it from its
+    own ``weight_g`` / ``weight_v`` (torch's weight_norm semantics), so the targets are exact
+    copies as the reference intends.  Nothing else of the reference is changed."""
+    orig = TD3_featured.copy
+
+    class _Copy:
+        @staticmethod
+        def deepcopy(m):
+            held = [(mod, mod.__dict__.pop("weight")) for mod in m.modules()
+                    if "weight_g" in mod._parameters and "weight" in mod.__dict__]
+            try:
+                return orig.deepcopy(m)
+            finally:
+                for mod, w in held:
+                    mod.__dict__["weight"] = w
+
+    TD3_featured.copy = _Copy
+    try:
+        yield
+    finally:
+        TD3_featured.copy = orig
+
+
 def make_featured(name, cfg, ref_mods, torch, F):
     sd, ad, ma, norm, B, steps, hp = cfg
     TD3_featured, my_rb = ref_mods
-    with contextlib.redirect_stdout(io.StringIO()):   # TD3_featured.py:103 prints params
+    wn = _weight_norm_deepcopy(TD3_featured) if norm == "weight_normalization" else contextlib.nullcontext()
+    with contextlib.redirect_stdout(io.StringIO()), wn:   # TD3_featured.py:103 prints params
         pol = TD3_featured.TD3(_Box((sd,)), _Box((ad,)), max_action=ma, norm=norm, **hp)
     ashapes = gen.featured_actor_shapes(sd, ad, norm)
     cshapes = gen.featured_critic_shapes(sd, ad, norm)

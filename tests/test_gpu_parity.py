@@ -134,7 +134,7 @@ def test_adam_moments_match_oracle():
         assert _rel_to_max(sda["state"][i]["exp_avg"].numpy(), L.actor_m[k]) <= 2e-4, k
 
 
-@pytest.mark.parametrize("name", ["hc_layer", "hc_none", "pend_layer"])
+@pytest.mark.parametrize("name", ["hc_layer", "hc_none", "pend_layer", "hc_wn"])
 def test_free_running_matches_golden(name):
     """Four free-running steps against the reference's own goldens."""
     G = load_golden("featured", name)
@@ -185,7 +185,7 @@ def test_select_action_and_eval_q():
         np.testing.assert_allclose(q[1], q2[0], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("name", ["hc_layer", "hc_none"])
+@pytest.mark.parametrize("name", ["hc_layer", "hc_none", "hc_wn"])
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 300])
 def test_select_action_eval_q_batch_paths(name, n):
     """The query paths of td3.hip: n <= 4 rows on the gemv chain (gemv_kernel<1, 2, 4>), up to 256
@@ -226,6 +226,31 @@ def test_select_action_eval_q_wide_input(n):
     for j, qn in enumerate(("q1", "q2")):
         qr, _ = orc.featured_q(S["critic"], qn, S["norm"], st, got)
         assert _rel_to_max(q[j * n:(j + 1) * n], qr[:, 0]) <= 1e-5
+
+
+def test_weight_norm_init_and_state_dict():
+    """norm="weight_normalization": the default init is torch's weight_norm(Linear) (g = ||W||
+    per row, v = W), the state dict has the reference's keys and shapes, and set / get round-trips
+    (g, v) exactly -- W itself is derived on the device (wn_kernel) and never exported."""
+    import torch
+    from td3_amd.TD3_featured import TD3
+    torch.manual_seed(3)
+    pol = TD3(Box((17,)), Box((6,)), norm="weight_normalization")
+    sd = pol.actor.state_dict()
+    assert list(sd)[:3] == ["linears.0.bias", "linears.0.weight_g", "linears.0.weight_v"]
+    assert tuple(sd["linears.0.weight_g"].shape) == (500, 1)
+    assert tuple(sd["linears.0.weight_v"].shape) == (500, 17)
+    assert not any("lnorms" in k for k in sd)
+    v = sd["linears.1.weight_v"].numpy().astype(np.float64)
+    np.testing.assert_allclose(sd["linears.1.weight_g"].numpy()[:, 0], np.linalg.norm(v, axis=1), rtol=1e-6)
+    rs = np.random.RandomState(0)
+    new = {k: rs.standard_normal(t.shape).astype(np.float32) for k, t in sd.items()}
+    pol.actor.load_state_dict(new)
+    for k, t in pol.actor.state_dict().items():
+        np.testing.assert_array_equal(t.numpy(), new[k])
+    s = rs.standard_normal(17).astype(np.float32)
+    ref = orc.featured_select_action(new, "weight_normalization", 1.0, s)
+    assert _rel_to_max(pol.select_action(s), ref) <= 1e-5
 
 
 def test_foreign_buffer_path():
@@ -290,13 +315,15 @@ def test_philox_noise_is_standard_normal():
     assert st.kstest(z, "norm").pvalue > 1e-4
 
 
-def test_allreduce_path_single_rank():
-    """The data-parallel kernels (grad-only dW, RCCL all-reduce, flat Adam + Polyak) at
-    nranks = 1 against the oracle, teacher-forced like the fused path."""
+@pytest.mark.parametrize("name", ["hc_layer", "hc_wn"])
+def test_allreduce_path_single_rank(name):
+    """The data-parallel kernels (grad-only dW, RCCL all-reduce, flat Adam + Polyak; with weight
+    normalization the all-reduced dW feeds wn_kernel) at nranks = 1 against the oracle,
+    teacher-forced like the fused path."""
     import ctypes as C
     from td3_amd import _lib
-    G = load_golden("featured", "hc_layer")
-    S = featured_setup("hc_layer")
+    G = load_golden("featured", name)
+    S = featured_setup(name)
     pol, rb = _make(S)
     uid = (C.c_ubyte * 128)()
     _lib.check(pol._lib.td3_comm_unique_id(uid), "td3_comm_unique_id")
