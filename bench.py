@@ -173,6 +173,8 @@ def main():
                     help="step launch mode: hipGraph replay, direct launches, or auto (replay while the "
                          "GPU has caught up with the host, direct launches while steps are queued)")
     ap.add_argument("--eager", action="store_true", help="same as --launch eager")
+    ap.add_argument("--norm", choices=["layer", "none", "weight_normalization"], default="layer",
+                    help="network normalisation (SURVEY §8d measures norm=layer; featured configs only)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     if args.eager:
@@ -203,8 +205,8 @@ def main():
         from td3_amd.TD3_featured import TD3
         from td3_amd.my_replay_buffer import ReplayBuffer_featured as RB
         obs = Box((cfg["sd"],))
-        pol = TD3(obs, Box((cfg["ad"],)), max_action=cfg["ma"], norm="layer", device=local,
-                  seed=17 + rank, use_graph=use_graph)
+        pol = TD3(obs, Box((cfg["ad"],)), max_action=cfg["ma"], device=local, seed=17 + rank,
+                  use_graph=use_graph, norm=None if args.norm == "none" else args.norm)
     rb = RB(obs, Box((cfg["ad"],)), max_size=REPLAY_ROWS, device=local, seed=101 + rank)
     rb.fill_synthetic(REPLAY_ROWS, cfg["ma"], seed=7 + rank)
     if world > 1:
@@ -281,7 +283,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "replay_per_gpu": REPLAY_ROWS,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "global_steps_per_s": round(gsteps, 3),
-                       "launch": args.launch},
+                       "launch": args.launch, "norm": args.norm},
         }
         if roof is not None:
             out["roofline"] = roof

@@ -311,16 +311,21 @@ __device__ __forceinline__ AdamK make_adam(const AdamArgs& a, const AdamPw& pw) 
 __device__ __forceinline__ AdamK make_adam(const AdamArgs& a) { return make_adam(a, adam_pw(a)); }
 
 // torch _single_tensor_adam (adam.py:520-547): lerp, mul/addcmul, sqrt/div/add, addcdiv.
-// Returns the updated (parameter, target); the target is 0 without Polyak.
-__device__ __forceinline__ float2 adam_elem(float* __restrict__ p, float* __restrict__ m,
-                                          float* __restrict__ v, float g, const AdamK& k,
-                                          float* __restrict__ t) {
-  float mm = gld(m), vv = gld(v), pp = gld(p);
+// One Adam update on values in registers (the arithmetic of adam_elem).
+__device__ __forceinline__ void adam_regs(float& pp, float& mm, float& vv, float g, const AdamK& k) {
   mm = __fmaf_rn(k.w1, g - mm, mm);
   vv = vv * k.b2;
   vv = vv + (k.c2 * g) * g;
   const float denom = sqrtf(vv) / k.bc2s + k.eps;
   pp = pp + (k.negss * mm) / denom;
+}
+
+// Returns the updated (parameter, target); the target is 0 without Polyak.
+__device__ __forceinline__ float2 adam_elem(float* __restrict__ p, float* __restrict__ m,
+                                          float* __restrict__ v, float g, const AdamK& k,
+                                          float* __restrict__ t) {
+  float mm = gld(m), vv = gld(v), pp = gld(p);
+  adam_regs(pp, mm, vv, g, k);
   gst(m, mm);
   gst(v, vv);
   gst(p, pp);

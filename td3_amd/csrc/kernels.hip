@@ -2132,11 +2132,26 @@ __global__ __launch_bounds__(256) void wn_kernel(WnArgs a) {
     return;
   }
   const AdamArgs& A = a.adam;
-  const AdamK k = make_adam(A);
-  float gw[8], vt[8];
-  rv_load(v, A.P + L.offv + (size_t)i * L.ld, L.K, lane);
+  float* T = a.polyak ? A.T : nullptr;
+  // every operand of the row requested up front: v, dW, the moments (and targets) of v, and on
+  // lane 0 g, the bias and their optimizer state
+  const size_t ov = L.offv + (size_t)i * L.ld;
+  float gw[8], m[8], w2[8], vt[8];
+  rv_load(v, A.P + ov, L.K, lane);
   rv_load(gw, A.G + L.offW + (size_t)i * L.ld, L.K, lane);
-  const float g = gld(A.P + L.offg + i);
+  rv_load(m, A.M + ov, L.K, lane);
+  rv_load(w2, A.V + ov, L.K, lane);
+  if (T) rv_load(vt, T + ov, L.K, lane);
+  const size_t og = L.offg + i, ob = L.offb + i;
+  float sg[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f}, gb = 0.f;
+  if (lane == 0) {
+    sg[0] = gld(A.P + og); sg[1] = gld(A.M + og); sg[2] = gld(A.V + og);
+    sb[0] = gld(A.P + ob); sb[1] = gld(A.M + ob); sb[2] = gld(A.V + ob);
+    gb = gld(A.G + ob);
+    if (T) { sg[3] = gld(T + og); sb[3] = gld(T + ob); }
+  }
+  const AdamK k = make_adam(A);
+  const float g = lane0(sg[0]);
 #pragma unroll
   for (int j = 0; j < 8; ++j) gw[j] *= k.gscale;
   const float n = wn_norm(v, L.K, lane);
@@ -2144,28 +2159,32 @@ __global__ __launch_bounds__(256) void wn_kernel(WnArgs a) {
   const float ca = g / n;
   const float cb = ca * sdot / (n * n);
   const float dg = sdot / n;
-  float* T = a.polyak ? A.T : nullptr;
-  // v: the lane's 8 columns, element-wise Adam; the updated values stay in registers
+  // v: element-wise Adam in registers (pads stay 0: zero grads and moments)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = rcol(lane, j);
-    vt[j] = 0.f;
-    if (c < L.K) {
-      const size_t o = L.offv + (size_t)i * L.ld + c;
-      const float2 u = adam_elem(A.P + o, A.M + o, A.V + o, ca * gw[j] - cb * v[j], k, T ? T + o : nullptr);
-      v[j] = u.x;
-      vt[j] = u.y;
-    } else {
-      v[j] = 0.f;
+    const float d = ca * gw[j] - cb * v[j];
+    if (rcol(lane, j) < L.K) {
+      adam_regs(v[j], m[j], w2[j], d, k);
+      if (T) vt[j] = k.tau * v[j] + k.omt * vt[j];        // TD3_featured.py:167-171
     }
   }
-  float2 ug = make_float2(0.f, 0.f);
+  rv_store(A.P + ov, L.K, lane, v);
+  rv_store(A.M + ov, L.K, lane, m);
+  rv_store(A.V + ov, L.K, lane, w2);
+  if (T) rv_store(T + ov, L.K, lane, vt);
   if (lane == 0) {
-    const size_t og = L.offg + i, ob = L.offb + i;
-    ug = adam_elem(A.P + og, A.M + og, A.V + og, dg, k, T ? T + og : nullptr);
-    (void)adam_elem(A.P + ob, A.M + ob, A.V + ob, gld(A.G + ob) * k.gscale, k, T ? T + ob : nullptr);
+    adam_regs(sg[0], sg[1], sg[2], dg, k);
+    adam_regs(sb[0], sb[1], sb[2], gb * k.gscale, k);
+    gst(A.P + og, sg[0]); gst(A.M + og, sg[1]); gst(A.V + og, sg[2]);
+    gst(A.P + ob, sb[0]); gst(A.M + ob, sb[1]); gst(A.V + ob, sb[2]);
+    if (T) {
+      sg[3] = k.tau * sg[0] + k.omt * sg[3];
+      sb[3] = k.tau * sb[0] + k.omt * sb[3];
+      gst(T + og, sg[3]);
+      gst(T + ob, sb[3]);
+    }
   }
-  const float gn = lane0(ug.x), gt = lane0(ug.y);
+  const float gn = lane0(sg[0]), gt = lane0(sg[3]);
   wn_store_w(A.P, L, i, lane, v, gn);
   if (T) wn_store_w(T, L, i, lane, vt, gt);
 }
