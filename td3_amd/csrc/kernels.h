@@ -28,6 +28,9 @@ enum Pro : int {
   kProL0 = 4,          // layer 0 (input width <= 32) recomputed for the workgroup's 32 rows on
                        // MFMA, ReLU, LayerNorm: the A rows of layer 1 (one launch for two layers)
   kProL0G = 5,         // kProL0 with the input rows sampled from the replay ring (as kProGather)
+  kProHeadBwd = 6,     // the actor loss's Q1 head backward (dU3 = -1/B w4 on every row): dZ3 =
+                       // relu'(LN3_bwd(dU3)) with LN3's statistics from the H3 rows themselves;
+                       // ex[3] = w4, ex[4] = b4, ex[5] = Q1 out (n-tile 0), exf[0] = -1/B
 };
 // kProL0 / kProL0G operand slots: ex[8] = W0 [N0p][32], ex[9] = b0, ex[10] = H0 out (nullable,
 // ld exi[5]), exi[5] = N0p (<= 512, the layer-1 Kp), exi[6] = K0 (input width, <= 32),

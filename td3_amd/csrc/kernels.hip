@@ -143,6 +143,77 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
   }
 }
 
+// The actor loss -mean Q1(s, pi(s)) (TD3_featured.py:159) backward into Q1's head as the prologue
+// of the first input-grad stage (kProHeadBwd): dL/dQ_r = -1/B for every live row, so dU3 = -w4/B
+// is the same row everywhere and each column-tile workgroup forms dZ3 of its 32 rows from H3
+// alone: LN3 statistics, Q1 = w4 . LN3(H3) + b4 (stored by n-tile 0 for the loss value), then
+// relu'(LN3_bwd(dU3)).  Row work is 3 wave reductions per row on top of pro_lnbwd's 2, so the
+// repetition over column tiles costs less than the row launch it replaces.
+__device__ __forceinline__ void pro_headbwd(const GemmProb& P, float* smem, const Ctx& c) {
+  constexpr int RB = 2;
+  float g[8], w[8], rm[8], bb[8];
+  rv_load(w, P.ex[3], P.Kp, c.lane);
+  if (P.norm) {
+    rv_load(g, P.lng, P.Kp, c.lane);
+    rv_load(bb, P.lnb, P.Kp, c.lane);
+  }
+  const float b4 = gld(P.ex[4]);
+  real_mask(rm, P.Kreal, c.lane);
+  const float invK = 1.0f / (float)P.Kreal;
+  const bool t0 = c.nt == 0;
+  float hall[kRPW][8];          // all of the wave's rows in one load round
+#pragma unroll
+  for (int r = 0; r < kRPW; ++r) rv_load(hall[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r) * P.lda, P.Kp, c.lane);
+#pragma unroll
+  for (int r0 = 0; r0 < kRPW; r0 += RB) {
+    float h[RB][8], gu[RB][8], mean[RB], rstd[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[r][j] = hall[r0 + r][j];
+    if (P.norm) {   // LN3 statistics (ln_fwd_rows_pk's two passes; the normalised row is not needed)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const f32x2 a = (pk2(h[r], 0) + pk2(h[r], 1)) + (pk2(h[r], 2) + pk2(h[r], 3));
+        mean[r] = wsum(a.x + a.y) * invK;
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const f32x2 nm = splat2(-mean[r]);
+        f32x2 v = splat2(0.f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 d = pkfma(nm, pk2(rm, q), pk2(h[r], q));
+          v = pkfma(d, d, v);
+        }
+        rstd[r] = __builtin_amdgcn_rsqf(wsum(v.x + v.y) * invK + 1e-5f);
+      }
+    }
+    if (t0) {       // Q1 = w4 . LN3(H3) + b4, for the loss value
+      float x[RB][8];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const float nb = -mean[r] * rstd[r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          x[r][j] = P.norm ? __fmaf_rn(__fmaf_rn(h[r][j], rstd[r], nb), g[j], bb[j]) : h[r][j];
+        const float q = wsum(rv_pdot(x[r], w, P.Kreal, c.lane)) + b4;
+        if (c.lane == 0) gst(P.ex[5] + (c.m0 + c.wave * kRPW + r0 + r), q);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const float gq = c.m0 + c.wave * kRPW + r0 + r < P.B ? P.exf[0] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gu[r][j] = gq * w[j];
+    }
+    if (P.norm) ln_bwd_rows_pk<RB>(gu, h, g, mean, rstd, invK);
+    else ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.Kreal, c.lane, 0);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * kRPW + r0 + r, P.Kp, c.lane, gu[r]);
+  }
+}
+
 // Replay-ring rows (kProGather): the step's sample (my_replay_buffer.py:119-128) drawn and read
 // by the first layer itself.  Row indices: Philox(seed, total_it + 1, row) over [0, size), the
 // same draw as gather_kernel; padded rows (>= B) are zero.  Record fields are not 16-B aligned,
@@ -1142,9 +1213,14 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
                    "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
                    "s"(P.norm), "s"(P.B));
   } else {
-    asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.H), "s"(P.stats), "s"(P.Aout), "s"(P.W), "s"(P.bias),
-                 "s"(P.C), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.ldh), "s"(P.ldao), "s"(P.ldw), "s"(P.Nout),
-                 "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.hot_pad));
+    if constexpr (PRO == kProHeadBwd)      // one batch with the head operands (a second asm would be a
+      asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.W), "s"(P.C), "s"(P.lda), "s"(P.Kreal),
+                   "s"(P.Kp), "s"(P.ldw), "s"(P.Nout), "s"(P.ldc), "s"(P.ntiles), "s"(P.tile_begin),
+                   "s"(P.norm), "s"(P.B), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]), "s"(P.exf[0]));
+    else                                   // second dependent kernel-argument round trip)
+      asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.H), "s"(P.stats), "s"(P.Aout), "s"(P.W), "s"(P.bias),
+                   "s"(P.C), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.ldh), "s"(P.ldao), "s"(P.ldw), "s"(P.Nout),
+                   "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.hot_pad));
     if constexpr (PRO == kProGather)
       asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]),
                    "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
@@ -1233,6 +1309,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
   if constexpr (PRO == kProCopy) pro_copy<kRPW>(P, smem, c);
   else if constexpr (PRO == kProLN) pro_ln(P, smem, c, issue_stream);
   else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
+  else if constexpr (PRO == kProHeadBwd) pro_headbwd(P, smem, c);
   else if constexpr (PRO == kProGather) pro_gather(P, tab.rs, smem, c, pi);
   else if constexpr (kL0) {
     float* xs = smem + 32 * S;
@@ -2220,6 +2297,7 @@ static GemmFn pick_bwd(int pro) {
   switch (pro) {
     case kProCopy: return gl<1, WN, kProCopy>;
     case kProLNBwd: return gl<1, WN, kProLNBwd>;
+    case kProHeadBwd: return gl<1, WN, kProHeadBwd>;
   }
   return nullptr;
 }
@@ -2465,6 +2543,7 @@ static int set_attr_all() {
   TD3_ATTR(0, kProL0G);
   TD3_ATTR(1, kProCopy);
   TD3_ATTR(1, kProLNBwd);
+  TD3_ATTR(1, kProHeadBwd);
 #undef TD3_ATTR
   return 0;
 }

@@ -633,7 +633,7 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<BwdItem>& items, int Bp, int B, const char* tag,
                           bool need_dz0, bool need_in = false,
-                          std::vector<GemmProb>* lnbwd_rows = nullptr) {
+                          std::vector<GemmProb>* lnbwd_rows = nullptr, float head_bwd_scale = 0.f) {
   const bool norm = h->cfg.norm == 1;
   for (int l = 2; l >= (need_in ? 0 : 1); --l) {
     std::vector<GemmProb> probs;
@@ -652,7 +652,17 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       GemmProb p{};
       p.norm = norm ? 1 : 0;
       p.B = B;
-      if (l == 2) {                       // dZ2 rows come from the loss / head row kernel
+      if (l == 2 && head_bwd_scale != 0.f) {   // dZ2 formed from H2 by the prologue (kProHeadBwd)
+        const NetL& n = *it.net;
+        p.A = it.e->H[2];
+        p.lda = L.Np;
+        p.lng = it.P + n.ln[2].offg;
+        p.lnb = it.P + n.ln[2].offb;
+        p.ex[3] = const_cast<float*>(it.P + n.lin[3].offW);
+        p.ex[4] = const_cast<float*>(it.P + n.lin[3].offb);
+        p.ex[5] = it.e->Qv;
+        p.exf[0] = head_bwd_scale;
+      } else if (l == 2) {                // dZ2 rows come from the loss / head row kernel
         p.A = it.e->GZ[2];
         p.lda = L.Np;
       } else {
@@ -682,7 +692,8 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       lds = std::max(lds, gemm_lds_bytes(L.Np));
       probs.push_back(p);
     }
-    TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, l == 2 ? kProCopy : kProLNBwd, Bp, lds, blocks,
+    const int pro = l < 2 ? kProLNBwd : head_bwd_scale != 0.f ? kProHeadBwd : kProCopy;
+    TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, pro, Bp, lds, blocks,
                            flops, std::string(tag) + "_bwd" + std::to_string(l), nullptr, 0));
   }
   if (need_dz0 && !need_in && lnbwd_rows) {     // as row problems for a shared row launch (kRowLnBwd)
@@ -1170,26 +1181,10 @@ static int build_step(td3_handle* h, int B) {
       // ---------------- delayed policy update (TD3_featured.py:156-171)
       std::vector<FwdItem> f3 = {{&q1, Pq1, &P->AQ, false, true}};
       TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0, nullptr, nullptr, 0, true));
-      {
-        GemmProb p{};
-        p.norm = norm ? 1 : 0;
-        p.B = B;
-        p.ex[0] = P->AQ.H[2];
-        p.ex[1] = const_cast<float*>(Pq1 + q1.ln[2].offg);
-        p.ex[2] = const_cast<float*>(Pq1 + q1.ln[2].offb);
-        p.ex[3] = const_cast<float*>(Pq1 + q1.lin[3].offW);
-        p.ex[4] = const_cast<float*>(Pq1 + q1.lin[3].offb);
-        p.ex[5] = P->AQ.Qv;
-        p.Aout = P->AQ.GZ[2];
-        p.ldao = q1.lin[2].Np;
-        p.exi[0] = q1.lin[2].N;
-        p.exi[1] = q1.lin[2].Np;
-        p.exf[0] = (float)(-1.0) / (float)B;
-        std::vector<GemmProb> v = {p};
-        TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorLoss, Bp, "actor_loss"));
-      }
+      // the actor loss -mean Q1(s, pi(s)) (:159): Q1's head and its backward are the prologue of
+      // AQB_bwd2 (kProHeadBwd; the row launch kRowActorLoss is the particle path's)
       std::vector<BwdItem> aqb = {{&q1, Pq1, &P->AQ, false}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false));
+      TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false, false, nullptr, (float)(-1.0) / (float)B));
       {
         GemmProb p{};
         p.norm = norm ? 1 : 0;
