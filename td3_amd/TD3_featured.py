@@ -319,6 +319,17 @@ class TD3(TD3_base):
         check(self._lib.td3_eval_q(self._h, _lib.fptr(s), _lib.fptr(a), _lib.fptr(q), 1), "td3_eval_q")
         return [q[0:1].copy(), q[1:2].copy()]
 
+    def eval_q_batch(self, states, actions):
+        """``eval_q`` over n (state, action) rows at once: (Q1 [n], Q2 [n])."""
+        s = np.ascontiguousarray(np.asarray(states, dtype=np.float32).reshape(-1, self.state_dim))
+        a = np.ascontiguousarray(np.asarray(actions, dtype=np.float32).reshape(-1, self.action_dim))
+        if s.shape[0] != a.shape[0]:
+            raise ValueError("states and actions must have the same number of rows")
+        n = s.shape[0]
+        q = np.empty(2 * n, dtype=np.float32)
+        check(self._lib.td3_eval_q(self._h, _lib.fptr(s), _lib.fptr(a), _lib.fptr(q), n), "td3_eval_q")
+        return q[:n].copy(), q[n:].copy()
+
     def train(self, replay_buffer, batch_size=100):
         self.train_step(replay_buffer, batch_size)
 

@@ -33,8 +33,10 @@ def main():
     lib.td3_tl_read.restype = C.c_int
     lib.td3_tl_read.argtypes = [C.c_void_p, C.c_int]
     lib.td3_tl_clear.restype = C.c_int
-    lib.td3_clk_read.restype = C.c_int
-    lib.td3_clk_read.argtypes = [C.c_void_p, C.c_int]
+    has_clk = hasattr(lib, "td3_clk_read")     # builds with the shader-clock marks only
+    if has_clk:
+        lib.td3_clk_read.restype = C.c_int
+        lib.td3_clk_read.argtypes = [C.c_void_p, C.c_int]
     sd, ad, B = 17, 6, 256
     pol = TD3(Box((sd,)), Box((ad,)), max_action=1.0, norm="layer", device=0, seed=17, use_graph=False)
     rb = RB(Box((sd,)), Box((ad,)), max_size=100_000, device=0, seed=3)
@@ -86,7 +88,8 @@ def main():
             span = (t3.max() - base) * 0.01
             spread = (t0.max() - base) * 0.01
             clk = np.zeros((8192, 2), dtype=np.uint64)
-            lib.td3_clk_read(clk.ctypes.data, 8192)
+            if has_clk:
+                lib.td3_clk_read(clk.ctypes.data, 8192)
             ck = clk[(buf[:, 3] != 0)].astype(np.int64)
             dt_rt = (t2 - t1).astype(np.float64)
             ok = dt_rt > 20
