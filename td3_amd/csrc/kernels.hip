@@ -2043,6 +2043,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   __shared__ float sm[2 * 2 * 64 * kDw64S];         // [buf][operand][64 rows][kDw64S]
   __shared__ float4 ssl4[2][16];                     // SC: [buf] the 64 rows' dZ scales
   const int b = xcd_tile(nb);
+  TL_MARK(0);
   if (b >= nb) return;
   int pi = 0;
 #pragma unroll
@@ -2055,6 +2056,10 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   const AdamPw pw = adam_pw(a.adam);
   if (t >= nmat) {
     dw_vector_tile_cols<512, SC>(a, P, make_adam(a.adam, pw), t - nmat, sm);
+#ifdef TD3_TL
+    if (threadIdx.x == 0 && blockIdx.x < 8192) td3_tl[blockIdx.x][6] = 1;   // vector tile (tl_probe)
+#endif
+    TL_MARK(3);
     return;
   }
   const int kt = t % P.ntk, nt = t / P.ntk;
@@ -2125,6 +2130,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
     }
   }
   __syncthreads();                                   // staging buffers become the reduction tile
+  TL_MARK(1);
   float* red = sm + (wave & 3) * 32 * 33;
   if (rh == 1) {
 #pragma unroll
@@ -2146,7 +2152,9 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
       ok[r] = n < P.Np && kk < P.Kp;
       idx[r] = P.offW + (int64_t)n * P.Kp + kk;
     }
+    TL_MARK(2);
     apply_grads<16>(a, make_adam(a.adam, pw), idx, gq, ok);
+    TL_MARK(3);
   }
 }
 

@@ -37,10 +37,10 @@ def main():
     if has_clk:
         lib.td3_clk_read.restype = C.c_int
         lib.td3_clk_read.argtypes = [C.c_void_p, C.c_int]
-    sd, ad, B = 17, 6, 256
+    sd, ad, B = (int(x) for x in os.environ.get("TL_SHAPE", "17,6,256").split(","))   # e.g. 376,17,1024
     pol = TD3(Box((sd,)), Box((ad,)), max_action=1.0, norm="layer", device=0, seed=17, use_graph=False)
-    rb = RB(Box((sd,)), Box((ad,)), max_size=100_000, device=0, seed=3)
-    rb.fill_synthetic(100_000, 1.0, seed=7)
+    rb = RB(Box((sd,)), Box((ad,)), max_size=20_000 if sd > 64 else 100_000, device=0, seed=3)
+    rb.fill_synthetic(rb.max_size, 1.0, seed=7)
     for _ in range(20):
         pol.train(rb, B)
     pol.sync()
@@ -76,7 +76,7 @@ def main():
                         print(f"   mark{k} {np.median(v[:, k] - v[:, 0]) * 0.01:5.2f}", end="")
                 print()
                 continue
-            if "gemm_kernel" not in kern and not kern.startswith("td3::dw_kernel"):
+            if "gemm_kernel" not in kern and not kern.startswith("td3::dw"):
                 print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f}")
                 continue
             lib.td3_tl_clear()
@@ -104,7 +104,15 @@ def main():
             if t6.min() > 0:
                 fine += f" mark6 {np.median(t6 - t0) * 0.01:5.2f} mark7 {np.median(t7 - t0) * 0.01:5.2f}"
             print(fine)
-            if name in ("F_fwd1", "F_fwd01", "TF_fwd1", "TF_fwd01", "C_dw") and phase == 1:
+            if kern.startswith("td3::dw64"):
+                vec = v[:, 6] == 1
+                for nm, sel in (("vector", vec), ("matrix", ~vec)):
+                    if sel.any():
+                        print(f"   {nm:7s} tiles {sel.sum():4d}: entry p50/max "
+                              f"{np.median((v[sel, 0] - base)) * 0.01:6.2f} {(v[sel, 0] - base).max() * 0.01:6.2f}"
+                              f"  dur p50/max {np.median(v[sel, 3] - v[sel, 0]) * 0.01:6.2f} "
+                              f"{(v[sel, 3] - v[sel, 0]).max() * 0.01:6.2f}  end max {(v[sel, 3] - base).max() * 0.01:6.2f}")
+            if name in ("F_fwd1", "F_fwd01", "TF_fwd1", "TF_fwd01", "C_dw", "A_dw") and phase == 1:
                 xcc = v[:, 4] & 0xFFFF
                 hw = v[:, 4] >> 32
                 print("   per-XCC wg counts:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
