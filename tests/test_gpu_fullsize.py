@@ -1,0 +1,78 @@
+"""Parity at BASELINE.json's full single-GPU configurations.
+
+* C2: HalfCheetah shapes, a ring of 1e6 rows, batch 256 -- the bench workload;
+* C3: Humanoid shapes, a ring of 2e6 rows (6.2 GB of 772-float records), batch 1024.
+
+The ring is filled on the device (``fill_synthetic``: the SURVEY §8d distribution) and the
+production step runs: Philox index draw over the whole ring, target-smoothing noise drawn on
+the device, the sample fused into the first layer (C2) or gathered by its own kernel (C3).  The
+drawn rows are read back from the ring with those indices (a bit-exact gather,
+``test_sample_gather_bit_exact``) and the oracle replays the same step teacher-forced: y, Q,
+losses and every parameter group at the SURVEY §8c tolerances, one critic-only and one policy
+step.  Size-independent properties: the draw spans the ring (the largest of 256 uniform draws
+from 1e6 rows lies below 0.9e6 with probability 0.9^256), the indices are in range and the noise
+is finite with unit scale.
+"""
+import numpy as np
+import pytest
+
+from helpers import gen, orc
+from test_gpu_parity import Box, _load_oracle_state, _params_close, _rel_to_max
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("sd,ad,ma,rows,B", [(17, 6, 1.0, 1_000_000, 256), (376, 17, 0.4, 2_000_000, 1024)],
+                         ids=["c2_halfcheetah", "c3_humanoid"])
+def test_full_config_production_step(sd, ad, ma, rows, B):
+    from td3_amd.TD3_featured import TD3
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+    a0 = gen.init_params(gen.featured_actor_shapes(sd, ad, "layer"), gen.SEED)
+    c0 = gen.init_params(gen.featured_critic_shapes(sd, ad, "layer"), gen.SEED + 100)
+    pol = TD3(Box((sd,)), Box((ad,)), max_action=ma, norm="layer", init="none")
+    pol.set_weights(a0, c0)
+    rb = ReplayBuffer_featured(Box((sd,)), Box((ad,)), max_size=rows, seed=5)
+    rb.fill_synthetic(rows, max_action=ma, seed=9)
+    assert (rb.ptr, rb.size) == (0, rows)
+    L = orc.Learner(a0, c0, max_action=ma, norm="layer")
+    for step in (1, 2):                                       # critic-only, then a policy step
+        _load_oracle_state(pol, L)
+        out = pol.train_step(rb, B, stats=True)
+        idx, noise = out["idx"], out["noise"]
+        assert idx.min() >= 0 and idx.max() < rows
+        assert idx.max() > 0.9 * rows
+        assert np.isfinite(noise).all() and 0.5 < noise.std() < 1.5
+        batch = tuple(t.cpu().numpy() for t in rb.sample(B, indices=idx))
+        rec = orc.featured_train_step(L, batch, noise)
+        assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5, step
+        assert _rel_to_max(out["q1"], rec["q1"][:, 0]) <= 1e-5, step
+        assert _rel_to_max(out["q2"], rec["q2"][:, 0]) <= 1e-5, step
+        np.testing.assert_allclose(out["critic_loss"], rec["critic_loss"], rtol=1e-5)
+        assert out["actor_step"] == ("actor_loss" in rec)
+        if out["actor_step"]:
+            np.testing.assert_allclose(out["actor_loss"], rec["actor_loss"], rtol=1e-5, atol=1e-7)
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (step, "critic"))
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (step, "critic_target"))
+        _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (step, "actor_target"))
+
+
+def test_full_ring_wraps():
+    """Adds into a full 1e6-row ring overwrite from ptr and wrap (my_replay_buffer.py:115-116):
+    after 1e6 synthetic rows and 1500 adds that straddle the end, ptr = 1500 - (1e6 - start) and
+    the overwritten rows read back exactly."""
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+    sd, ad, cap = 17, 6, 1_000_000
+    rb = ReplayBuffer_featured(Box((sd,)), Box((ad,)), max_size=cap)
+    rb.fill_synthetic(cap, max_action=1.0, seed=3)            # ptr wraps to 0, size = cap
+    s, a, s2, r, d = gen.fill_featured_buffer(sd, ad, 1.0, cap - 700 + 1500, 4)
+    rb.add_batch(s[:cap - 700], a[:cap - 700], s2[:cap - 700], r[:cap - 700], d[:cap - 700])
+    assert (rb.ptr, rb.size) == (cap - 700, cap)
+    for i in range(cap - 700, cap - 700 + 1500):              # single adds across the ring's end
+        rb.add(s[i], a[i], s2[i], r[i], d[i])
+    assert (rb.ptr, rb.size) == (800, cap)
+    idx = np.concatenate([np.arange(cap - 700, cap), np.arange(0, 800)])
+    got = rb.sample(len(idx), indices=idx)
+    src = np.arange(cap - 700, cap - 700 + 1500)
+    for g, want in zip(got, (s[src], a[src], s2[src], r[src][:, None], 1.0 - d[src][:, None])):
+        np.testing.assert_array_equal(g.cpu().numpy(), np.asarray(want, np.float32))
