@@ -29,7 +29,13 @@
  * Streams: `stream` arguments are hipStream_t passed as void*; NULL selects the
  * handle's own stream.  td3_train_step orders itself after the ring's last
  * rb_add / rb_fill_synthetic (a transition added at step t is samplable at t,
- * main.py:261 before :269).  Handles are not re-entrant.
+ * main.py:261 before :269), and a later write after the steps that read the ring.
+ * The ordering is recorded lazily (replay.h Ring::read_stream): accesses on one
+ * stream need no events, an access on another stream records one on the stream
+ * the ring last noted.  A caller stream passed to these calls must therefore stay
+ * alive until the ring's next access on another stream, or until rb_destroy;
+ * td3_destroy releases the handle's own streams from every ring.  Handles are not
+ * re-entrant.
  */
 #ifndef TD3_HIP_H
 #define TD3_HIP_H

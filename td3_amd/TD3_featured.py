@@ -352,7 +352,7 @@ class TD3(TD3_base):
         if noise is not None:
             nz = np.ascontiguousarray(np.asarray(noise, dtype=np.float32).reshape(B, self.action_dim))
         if isinstance(replay_buffer, ReplayBuffer_featured):
-            replay_buffer.flush()
+            replay_buffer.flush(self._lib.td3_stream(self._h))   # in the step's stream order
             ix = None
             if indices is not None:
                 ix = np.ascontiguousarray(np.asarray(indices, dtype=np.int64).reshape(B))

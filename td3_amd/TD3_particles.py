@@ -185,7 +185,7 @@ class TD3(_FeaturedTD3):
         if noise is not None:
             nz = np.ascontiguousarray(np.asarray(noise, dtype=np.float32).reshape(B, A))
         if isinstance(replay_buffer, ReplayBuffer_particles):
-            replay_buffer.flush()
+            replay_buffer.flush(self._lib.td3_stream(self._h))   # in the step's stream order
             ix = None
             if indices is not None:
                 ix = np.ascontiguousarray(np.asarray(indices, dtype=np.int64).reshape(B))

@@ -27,28 +27,35 @@ struct Ring {
   uint64_t sample_calls = 0;       // Philox counter of the stand-alone sample()
   int device = 0;
   hipStream_t stream = nullptr;
-  float* stage[2] = {nullptr, nullptr};     // pinned host staging for add(), double-buffered
-  float* stage_dev[2] = {nullptr, nullptr}; // their device addresses (small adds read them in place)
+  float* stage[2] = {nullptr, nullptr};     // pinned host staging for large adds, double-buffered
+  float* stage_dev[2] = {nullptr, nullptr}; // their device addresses
   size_t stage_cap[2] = {0, 0};
   hipEvent_t stage_buf_ev[2] = {nullptr, nullptr};  // the write out of stage[i] finished
   int stage_cur = 0;
-  hipEvent_t stage_ev = nullptr;   // recorded after writes that use no staging buffer
-  hipEvent_t last_write = nullptr; // the last write (records + d_size), stage_ev or a stage_buf_ev:
-                                   // readers wait on it
-  // Ordering of writes after reads.  Every reader (a learner step, a stand-alone sample) records
-  // read_ev on its stream after the work that reads the records or d_size; a later write waits on
-  // it, so a step in flight never sees d_size or a record change under it.  Readers on different
-  // streams are chained (the new reader waits on read_ev first), so read_ev covers them all.
-  hipEvent_t read_ev = nullptr;
-  const void* read_stream = nullptr;        // stream of the last read_ev record (compared only)
+  // Ordering between the streams that read (a learner step, a stand-alone sample) and write
+  // (adds, fills) the ring, recorded lazily: an access only notes its stream; an access on ANOTHER
+  // stream records an event on the noted stream at that moment (covering everything queued there
+  // so far) and waits on it.  Accesses on one stream need nothing (stream order), so a learner
+  // that also flushes the adds on its own stream records no event per step -- a record is a
+  // marker packet that drains the queue: ~4 us of GPU time per step (C2 9.60k vs 9.97k steps/s).
+  // Readers are chained (a reader on a new stream waits on the previous one's), so the last
+  // read stream covers them all; writes likewise.
+  hipStream_t read_stream = nullptr, write_stream = nullptr;
+  bool reads_pending = false, writes_pending = false;
+  // the stream already ordered after the current reads / writes (nothing to wait for again)
+  hipStream_t reads_seen_by = nullptr, writes_seen_by = nullptr;
+  hipEvent_t read_ev = nullptr, write_ev = nullptr;
   int64_t* d_idx = nullptr;        // last drawn indices (rows) of sample()
   int idx_cap = 0;
 };
 
-// Reader protocol (see Ring::read_ev): ring_begin_read before enqueuing reads on s (waits on
-// the last write and, on a new stream, on the previous readers), ring_end_read after them.
+// Reader protocol (Ring::read_stream): ring_begin_read before enqueuing reads on s (orders them
+// after the writes and the earlier readers of other streams), ring_end_read after them.
 int ring_begin_read(Ring* r, hipStream_t s);
 int ring_end_read(Ring* r, hipStream_t s);
+// A stream that is about to be destroyed (synchronised by the caller) stops being a ring's
+// noted reader / writer.
+void ring_forget_stream(hipStream_t s);
 
 // One gather destination: rows [0, Bp) of dst[r*ld + col + c] = record[src + c], c < len.
 struct GatherSeg {

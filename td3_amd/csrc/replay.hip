@@ -11,6 +11,8 @@
 #include <string.h>
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <set>
 
 #include "replay.h"
 #include "../../include/td3.h"
@@ -127,15 +129,66 @@ __global__ __launch_bounds__(256) void ring_put_kernel(float4* __restrict__ data
   if (blockIdx.x == 0 && threadIdx.x == 0) *d_size = new_size;
 }
 
+// Adds of a few records travel in the kernel arguments (no host staging buffer whose reuse would
+// need an event): rows [0, n) of `rows` (rec floats each) into ring rows ptr, ptr+1, .. (wrapping).
+constexpr int kPutArgFloats = 960;
+struct RingPutArgs {
+  float4* data;
+  int64_t* d_size;
+  int64_t cap, ptr, n, new_size;
+  int rec4;
+  float rows[kPutArgFloats];
+};
+__global__ __launch_bounds__(256) void ring_put_args_kernel(RingPutArgs a) {
+  const int64_t total = a.n * a.rec4;
+  for (int64_t i = threadIdx.x; i < total; i += 256) {
+    const int64_t row = i / a.rec4, c = i - row * a.rec4;
+    int64_t dst = a.ptr + row;
+    if (dst >= a.cap) dst -= a.cap;
+    a.data[dst * a.rec4 + c] = reinterpret_cast<const float4*>(a.rows)[i];
+  }
+  if (threadIdx.x == 0) *a.d_size = a.new_size;
+}
+
+// The lazy ordering of Ring::read_stream / write_stream: when `s` differs from the noted stream,
+// an event recorded there now (it covers everything queued so far) is waited on by `s`.
+static int order_after(hipStream_t s, hipStream_t noted, bool pending, hipEvent_t ev, hipStream_t& seen_by) {
+  if (!pending || !noted || noted == s || seen_by == s) return 0;
+  TD3_HIP(hipEventRecord(ev, noted));
+  TD3_HIP(hipStreamWaitEvent(s, ev, 0));
+  seen_by = s;
+  return 0;
+}
+
+static std::mutex g_rings_mu;
+static std::set<Ring*> g_rings;
+
+void ring_forget_stream(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_rings_mu);
+  for (Ring* r : g_rings) {
+    if (r->read_stream == s) {
+      r->read_stream = nullptr;
+      r->reads_pending = false;
+    }
+    if (r->write_stream == s) {
+      r->write_stream = nullptr;
+      r->writes_pending = false;
+    }
+    if (r->reads_seen_by == s) r->reads_seen_by = nullptr;
+    if (r->writes_seen_by == s) r->writes_seen_by = nullptr;
+  }
+}
+
 int ring_begin_read(Ring* r, hipStream_t s) {
-  TD3_HIP(hipStreamWaitEvent(s, r->last_write, 0));
-  if (r->read_stream && r->read_stream != (const void*)s) TD3_HIP(hipStreamWaitEvent(s, r->read_ev, 0));
+  TD3_RC(order_after(s, r->write_stream, r->writes_pending, r->write_ev, r->writes_seen_by));  // adds so far
+  TD3_RC(order_after(s, r->read_stream, r->reads_pending, r->read_ev, r->reads_seen_by));     // chained readers
   return 0;
 }
 
 int ring_end_read(Ring* r, hipStream_t s) {
-  TD3_HIP(hipEventRecord(r->read_ev, s));
   r->read_stream = s;
+  r->reads_pending = true;
+  r->reads_seen_by = nullptr;
   return 0;
 }
 
@@ -167,10 +220,13 @@ static int ring_alloc(Ring* r, int64_t max_size, int device, uint64_t seed, rb_h
   // finish them before any add / sample can be queued
   TD3_HIP(hipDeviceSynchronize());
   TD3_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-  TD3_HIP(hipEventCreateWithFlags(&r->stage_ev, hipEventDisableTiming));
-  r->last_write = r->stage_ev;
-  TD3_HIP(hipEventCreateWithFlags(&r->read_ev, hipEventDisableTiming));
-  for (auto& ev : r->stage_buf_ev) TD3_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  TD3_HIP(hipEventCreateWithFlags(&r->write_ev, TD3_EV_FLAGS));
+  TD3_HIP(hipEventCreateWithFlags(&r->read_ev, TD3_EV_FLAGS));
+  for (auto& ev : r->stage_buf_ev) TD3_HIP(hipEventCreateWithFlags(&ev, TD3_EV_FLAGS));
+  {
+    std::lock_guard<std::mutex> lk(g_rings_mu);
+    g_rings.insert(r);
+  }
   *out = reinterpret_cast<rb_handle*>(r);
   return 0;
 }
@@ -222,8 +278,12 @@ int rb_destroy(rb_handle* h) {
   if (!h) return 0;
   Ring* r = reinterpret_cast<Ring*>(h);
   (void)hipSetDevice(r->device);
-  (void)hipStreamSynchronize(r->stream);
-  if (r->read_stream) (void)hipEventSynchronize(r->read_ev);   // no reader still in flight
+  {
+    std::lock_guard<std::mutex> lk(g_rings_mu);
+    g_rings.erase(r);
+  }
+  // no reader or writer of the ring still in flight, whatever stream it was queued on
+  (void)hipDeviceSynchronize();
   (void)hipFree(r->data);
   (void)hipFree(r->d_size);
   (void)hipFree(r->d_idx);
@@ -232,7 +292,7 @@ int rb_destroy(rb_handle* h) {
     if (r->stage[i]) (void)hipHostFree(r->stage[i]);
     (void)hipEventDestroy(r->stage_buf_ev[i]);
   }
-  (void)hipEventDestroy(r->stage_ev);
+  (void)hipEventDestroy(r->write_ev);
   (void)hipEventDestroy(r->read_ev);
   (void)hipStreamDestroy(r->stream);
   delete r;
@@ -288,19 +348,18 @@ static int stage_index(const Ring* r, const float* host) {
   return -1;
 }
 
-// Writes (records, d_size) on `stream` start after every read queued so far (Ring::read_ev).
+// Writes (records, d_size) on `stream` start after every read and every other-stream write queued
+// so far (Ring::read_stream / write_stream).
 static int ring_begin_write(Ring* r, hipStream_t stream) {
-  if (r->read_stream && r->read_stream != (const void*)stream)
-    TD3_HIP(hipStreamWaitEvent(stream, r->read_ev, 0));
+  TD3_RC(order_after(stream, r->read_stream, r->reads_pending, r->read_ev, r->reads_seen_by));
+  TD3_RC(order_after(stream, r->write_stream, r->writes_pending, r->write_ev, r->writes_seen_by));
   return 0;
 }
 
-// `ev`: the event that marks this write (a staging buffer's, which then also frees the buffer),
-// or nullptr for the ring's own.
-static int ring_end_write(Ring* r, hipStream_t stream, hipEvent_t ev = nullptr) {
-  if (!ev) ev = r->stage_ev;
-  TD3_HIP(hipEventRecord(ev, stream));
-  r->last_write = ev;
+static int ring_end_write(Ring* r, hipStream_t stream) {
+  r->write_stream = stream;
+  r->writes_pending = true;
+  r->writes_seen_by = nullptr;
   return 0;
 }
 
@@ -321,6 +380,22 @@ static int push_staged(Ring* r, const float* host, int64_t n, hipStream_t stream
     r->size = r->cap;
   }
   const int64_t new_size = std::min<int64_t>(r->size + n, r->cap);
+  if ((int64_t)n * r->rec <= kPutArgFloats) {       // the records in the kernel arguments
+    RingPutArgs pa;
+    pa.data = reinterpret_cast<float4*>(r->data);
+    pa.d_size = r->d_size;
+    pa.cap = r->cap;
+    pa.ptr = r->ptr;
+    pa.n = n;
+    pa.new_size = new_size;
+    pa.rec4 = r->rec / 4;
+    memcpy(pa.rows, host + (size_t)skip * r->rec, (size_t)n * r->rec * sizeof(float));
+    hipLaunchKernelGGL(ring_put_args_kernel, dim3(1), dim3(256), 0, stream, pa);
+    TD3_HIP(hipGetLastError());
+    r->ptr = (r->ptr + n) % r->cap;
+    r->size = new_size;
+    return ring_end_write(r, stream);
+  }
   if (si >= 0 && (size_t)n * r->rec * sizeof(float) <= kPutKernelBytes) {
     const int64_t total4 = n * (r->rec / 4);
     const int grid = (int)std::min<int64_t>((total4 + 255) / 256, 256);
@@ -342,7 +417,8 @@ static int push_staged(Ring* r, const float* host, int64_t n, hipStream_t stream
     TD3_HIP(hipGetLastError());
   }
   r->size = new_size;
-  return ring_end_write(r, stream, si >= 0 ? r->stage_buf_ev[si] : nullptr);
+  if (si >= 0) TD3_HIP(hipEventRecord(r->stage_buf_ev[si], stream));   // the staging buffer is free
+  return ring_end_write(r, stream);
 }
 
 int rb_add(rb_handle* h, const double* state, const double* action, const double* next_state,
@@ -354,7 +430,9 @@ int rb_add(rb_handle* h, const double* state, const double* action, const double
   Ring* r = reinterpret_cast<Ring*>(h);
   TD3_ARG(!r->particles, "rb_add on a particle ring (use rb_add_particles)");
   TD3_HIP(hipSetDevice(r->device));
-  float* stage = ensure_stage(r, (size_t)n * r->rec);
+  float small[kPutArgFloats];                      // few records: packed here, shipped as launch arguments
+  const bool few = n * r->rec <= kPutArgFloats;
+  float* stage = few ? small : ensure_stage(r, (size_t)n * r->rec);
   if (!stage) return -2;
   for (int64_t i = 0; i < n; ++i) {
     float* d = stage + (size_t)i * r->rec;
@@ -404,10 +482,11 @@ int rb_add_records(rb_handle* h, const float* records, int64_t n, void* stream) 
   TD3_ARG(records != nullptr, "null records");
   Ring* r = reinterpret_cast<Ring*>(h);
   TD3_HIP(hipSetDevice(r->device));
+  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
+  if (n * r->rec <= kPutArgFloats) return push_staged(r, records, n, s);   // launch arguments
   float* stage = ensure_stage(r, (size_t)n * r->rec);
   if (!stage) return -2;
   memcpy(stage, records, (size_t)n * r->rec * sizeof(float));
-  hipStream_t s = stream ? (hipStream_t)stream : r->stream;
   return push_staged(r, stage, n, s);
 }
 
@@ -532,6 +611,8 @@ int rb_sync(rb_handle* h) {
   Ring* r = reinterpret_cast<Ring*>(h);
   TD3_HIP(hipSetDevice(r->device));
   TD3_HIP(hipStreamSynchronize(r->stream));
+  if (r->write_stream) TD3_HIP(hipStreamSynchronize(r->write_stream));   // adds flushed by a learner
+  if (r->read_stream) TD3_HIP(hipStreamSynchronize(r->read_stream));
   return 0;
 }
 

@@ -308,7 +308,11 @@ struct td3_handle {
   // last step that changed the online actor, so on critic-only steps (total_it % policy_freq != 0)
   // it overlaps the training step instead of queueing behind it.
   hipStream_t act_stream = nullptr;
-  hipEvent_t actor_ev = nullptr;              // recorded after every actor-updating step
+  hipEvent_t actor_ev = nullptr;              // recorded after every actor-updating step once a
+                                              // query ran (act_used): an event record costs the
+                                              // step's stream ~4 us, pure training needs none
+  bool act_used = false;
+  hipStream_t last_step_stream = nullptr;     // the stream of the last train step
   std::unique_ptr<Plan> plan;
   std::map<int, std::unique_ptr<ActPlan>> act;
   ncclComm_t comm = nullptr;
@@ -1700,11 +1704,13 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
   // use_graph 2 (auto): a hipGraph replay costs ~8 us of GPU time on top of its kernels
   // (tools/launch_floor.hip) but little host time; direct launches cost the host ~3 us each and
   // the GPU nothing extra.  While the last policy step is still queued the host is ahead of the
-  // GPU, so its launch time is hidden: launch directly.  Otherwise (host-bound loops) replay.
+  // GPU, so its launch time is hidden: launch directly.  Otherwise (host-bound acting loops: the
+  // last policy step has finished) replay.  Without queries (act_used: no actor event to ask;
+  // asking the stream queues a marker, a per-step drain) training launches directly.
   // Data parallel (RCCL comm attached): auto launches directly, so every rank issues its
   // all-reduces the same way whatever its local progress (no captured / uncaptured mix).
   const bool graph = h->cfg.use_graph == 1 ||
-                     (h->cfg.use_graph == 2 && !h->comm && !actor_phase &&
+                     (h->cfg.use_graph == 2 && !h->comm && !actor_phase && h->act_used &&
                       hipEventQuery(h->actor_ev) != hipErrorNotReady);
   if (!graph) {
     if (ring && !fused) TD3_RC(input_from_ring(h, ring, P, false, s));
@@ -1782,9 +1788,10 @@ static int bind_ring(td3_handle* h, Ring* r) {
 static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_stats* stats) {
   h->total_it += 1;
   h->critic_step += 1;
+  h->last_step_stream = s;
   if (actor_phase) {
     h->actor_step += 1;
-    TD3_HIP(hipEventRecord(h->actor_ev, s));
+    if (h->act_used) TD3_HIP(hipEventRecord(h->actor_ev, s));
   }
   if (!stats) return 0;
   Plan* P = h->plan.get();
@@ -2209,7 +2216,7 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_HIP(hipDeviceSynchronize());          // null-stream memsets vs the handle's non-blocking streams
   TD3_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   TD3_HIP(hipStreamCreateWithFlags(&h->act_stream, hipStreamNonBlocking));
-  TD3_HIP(hipEventCreateWithFlags(&h->actor_ev, hipEventDisableTiming));
+  TD3_HIP(hipEventCreateWithFlags(&h->actor_ev, TD3_EV_FLAGS));
   *out = h;
   return 0;
 }
@@ -2219,6 +2226,7 @@ int td3_destroy(td3_handle* h) {
   (void)hipSetDevice(h->cfg.device);
   (void)hipStreamSynchronize(h->stream);
   (void)hipStreamSynchronize(h->act_stream);
+  ring_forget_stream(h->stream);        // rings that noted it as their reader / writer
   if (h->plan) destroy_plan(h->plan.get());
   for (auto& kv : h->act) {
     free_plan_tables(kv.second->tables);
@@ -2490,6 +2498,18 @@ static int run_gemv(const ActPlan* A, bool q, int n, const float* x0, int c0, co
   return launch_heads(head, nprob, s);
 }
 
+// Queries wait for the last actor-updating step only (critic-only steps leave the actor as it
+// is).  The first query of a learner has no such event yet: it waits on everything its last step
+// stream has queued, and from then on every policy step records actor_ev.
+static int order_after_actor(td3_handle* h, hipStream_t s) {
+  if (!h->act_used) {
+    h->act_used = true;
+    if (h->last_step_stream) TD3_HIP(hipEventRecord(h->actor_ev, h->last_step_stream));
+  }
+  TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
+  return 0;
+}
+
 int td3_select_action(td3_handle* h, const float* state, float* action_out, int n) {
   TD3_ARG(h && state && action_out, "null argument");
   TD3_ARG(!h->particles, "particle learner: use td3_select_action_particles");
@@ -2499,7 +2519,7 @@ int td3_select_action(td3_handle* h, const float* state, float* action_out, int 
   TD3_RC(build_act(h, pad32(n), &A));
   hipStream_t s = h->act_stream;
   if (A->hio) TD3_HIP(hipStreamSynchronize(s));
-  TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
+  TD3_RC(order_after_actor(h, s));
   if (A->gemv && n <= kGemvRows) {
     if (!A->gemv01) TD3_RC(put_rows(A, A->X_S, A->hX_S, pad32(h->sd), 0, state, n, h->sd, s));
     TD3_RC(run_gemv(A, false, n, state, h->sd, nullptr, 0, s));
@@ -2584,7 +2604,7 @@ int td3_select_action_particles(td3_handle* h, const float* feat, const float* p
   TD3_RC(build_act_particles(h, pad32(n), &A));
   hipStream_t s = h->act_stream;
   if (A->hio) TD3_HIP(hipStreamSynchronize(s));
-  TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
+  TD3_RC(order_after_actor(h, s));
   const int np = h->N * h->D;
   const NetL& an = h->actor.nets[0];
   TD3_RC(put_rows(A, A->X_S, A->hX_S, an.lin[0].Kp, kEncC2, feat, n, h->sd, s));

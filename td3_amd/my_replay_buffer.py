@@ -51,11 +51,13 @@ def _new_stage(buf, rows):
     buf._n = 0
 
 
-def _flush_stage(buf):
+def _flush_stage(buf, stream=None):
+    """Ship the staged records; ``stream`` (a learner's, from ``TD3.train``) queues them in that
+    stream's order, so the step that samples them needs no cross-stream event (replay.h)."""
     n = buf._n
     if n:
         buf._n = 0
-        check(buf._lib.rb_add_records(buf._h, buf._stage_ptr, n, None), "rb_add_records")
+        check(buf._lib.rb_add_records(buf._h, buf._stage_ptr, n, stream), "rb_add_records")
 
 
 class _SafeIntUnpickler(pickle.Unpickler):
@@ -185,8 +187,8 @@ class ReplayBuffer_featured(object):
         check(self._lib.rb_add(self._h, _lib.dptr(s), _lib.dptr(a), _lib.dptr(s2), _lib.dptr(r),
                                _lib.dptr(d), n, self._stream()), "rb_add")
 
-    def flush(self):
-        _flush_stage(self)
+    def flush(self, stream=None):
+        _flush_stage(self, stream)
 
     def fill_synthetic(self, n, max_action=1.0, seed=0):
         """Device-side prefill with the SURVEY §8(d) synthetic distribution (bench/tests)."""
@@ -388,8 +390,8 @@ class ReplayBuffer_particles(object):
         check(self._lib.rb_add_particles(self._h, *[_lib.dptr(x) for x in arrs], n, self._stream()),
               "rb_add_particles")
 
-    def flush(self):
-        _flush_stage(self)
+    def flush(self, stream=None):
+        _flush_stage(self, stream)
 
     def fill_synthetic(self, n, max_action=1.0, seed=0):
         self.flush()
