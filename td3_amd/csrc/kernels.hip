@@ -1849,11 +1849,10 @@ __device__ __forceinline__ void dw_vector_tile_cols(const DwArgs& a, const DwPro
 // then the optimizer update of those 32 columns.  A thread owns 4 adjacent columns (float4 loads)
 // of every (NT/8)-th row: at Bp = 256 all of a thread's rows are requested in one batch, and the
 // optimizer state of the 32 x 3 elements is requested behind them.
-template <int NT, bool SC>
+template <int NT, bool SC, int U = 8>               // U: rows per group and batch
 __device__ __forceinline__ void dw_vector_tile(const DwArgs& a, const DwProb& P, const AdamPw& pw, int j,
                                                float* red) {
   constexpr int RG = NT / 8;                        // row groups
-  constexpr int U = 8;                              // rows per group and batch
   const int n0 = j * 32;
   const int c4 = (threadIdx.x & 7) * 4, rg = threadIdx.x >> 3;
   const bool ln = P.offg >= 0;
@@ -2038,6 +2037,9 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
 // at B >= 512.  The two row halves meet in LDS; the rh=0 waves apply the optimizer update.
 constexpr int kDw64S = 66;                          // LDS row stride: rows 16 apart 32 banks apart
 constexpr int kDw64Depth = 2;                       // 64-row steps in flight (1, 3, 5: no change)
+#ifndef TD3_DW64_VEC4
+#define TD3_DW64_VEC4 1
+#endif
 template <bool SC>
 __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   __shared__ float sm[2 * 2 * 64 * kDw64S];         // [buf][operand][64 rows][kDw64S]
@@ -2055,7 +2057,11 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   const int nmat = ntn * P.ntk;                      // ntk = k tiles of 64 in this mode
   const AdamPw pw = adam_pw(a.adam);
   if (t >= nmat) {
+#if TD3_DW64_VEC4
+    dw_vector_tile<512, SC, 4>(a, P, pw, t - nmat, sm);   // 4-row batches: <= 128 VGPRs
+#else
     dw_vector_tile_cols<512, SC>(a, P, make_adam(a.adam, pw), t - nmat, sm);
+#endif
 #ifdef TD3_TL
     if (threadIdx.x == 0 && blockIdx.x < 8192) td3_tl[blockIdx.x][6] = 1;   // vector tile (tl_probe)
 #endif
@@ -2111,8 +2117,10 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
       const int st = st0 + d;
       if (st >= nstep) break;
       const int buf = st & 1;
+#ifndef TD3_X_NOSTAGE
       put(buf, sg[d], su[d], ssc[d]);
       __syncthreads();
+#endif
       if (st + D < nstep) fetch((st + D) * 64, sg[d], su[d], ssc[d]);
       const float* g = sm + buf * 2 * 64 * kDw64S + (rh * 32 + 16 * h) * kDw64S;
       const float* uu = g + 64 * kDw64S;
@@ -2125,7 +2133,11 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
 #pragma unroll
       for (int s2 = 0; s2 < 16; ++s2) {
         const float ga = g[s2 * kDw64S + qn * 32 + i];
+#ifdef TD3_X_NOMFMA
+        acc[s2] += ga * uu[s2 * kDw64S + qk * 32 + i];
+#else
         acc = mfma32x32x2(SC ? ga * scl[s2] : ga, uu[s2 * kDw64S + qk * 32 + i], acc);
+#endif
       }
     }
   }
@@ -2140,6 +2152,143 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   // (the optimizer state is requested here, not behind the first operand steps: there its 64
   // loads per lane sat in front of the later steps' operand loads in the in-order vmcnt queue,
   // Humanoid C_dw 49 -> 60 us)
+  if (rh == 0) {
+    const int kk = k0 + qk * 32 + i;
+    int64_t idx[16];
+    float gq[16];
+    bool ok[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + qn * 32 + mfma_row(r, lane);
+      gq[r] = acc[r] + red[mfma_row(r, lane) * 33 + i];
+      ok[r] = n < P.Np && kk < P.Kp;
+      idx[r] = P.offW + (int64_t)n * P.Kp + kk;
+    }
+    TL_MARK(2);
+    apply_grads<16>(a, make_adam(a.adam, pw), idx, gq, ok);
+    TL_MARK(3);
+  }
+}
+
+// dw64_kernel with the operand steps staged by LDS-DMA (global_load_lds_dwordx4: no register
+// round trip, no LDS-write pass) when Bp is a multiple of 64.  LDS image per buffer and operand:
+// [64 rows][64 cols] unpadded, the two 32-column halves swapped on rows with bit 4 set (the DMA
+// destination is lane-linear, so the swizzle is applied to the per-lane SOURCE column; an MFMA
+// operand read takes rows 16 apart in its two lane halves, which then hit the other 32 banks).
+// Columns past Np / Kp are read from a clamped valid column: they only feed outputs the
+// epilogue masks.  One step is in flight while the previous one is multiplied.
+typedef __attribute__((address_space(3))) void* td3_lptr;
+// The DMA is issued by inline asm: through the builtin, hipcc cannot tell which LDS buffer a DMA
+// writes and waits vmcnt(0) before the first operand read of every step (draining the next
+// step's DMA); the waits are therefore placed by hand (vmcnt(0) before each step's barrier).
+__device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(td3_lptr)lds_wave_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+}
+__device__ __forceinline__ void glds4(const float* src, float* lds_wave_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(td3_lptr)lds_wave_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+}
+template <bool SC>
+// (launch bounds: 2 workgroups per CU, <= 128 VGPRs)
+__global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
+  // ONE __shared__ object (a second one made hipcc drain the DMA, vmcnt(0), before the first
+  // operand read of every step): [buf][operand][64 rows][64 cols (swizzled)], then SC's
+  // [buf][64] row scales
+  __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64];
+  float* const ssl = sm + 2 * 2 * 64 * 64;
+  const int b = xcd_tile(nb);
+  TL_MARK(0);
+  if (b >= nb) return;
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxDwProbs; ++i)
+    if (i < a.nprob && b >= a.probs[i].tile_begin) pi = i;
+  const DwProb& P = a.probs[pi];
+  const int t = b - P.tile_begin;
+  const int nmat = ((P.Np + 63) >> 6) * P.ntk;       // ntk = k tiles of 64 in this mode
+  const AdamPw pw = adam_pw(a.adam);
+  if (t >= nmat) {
+    dw_vector_tile<512, SC, 4>(a, P, pw, t - nmat, sm);   // 4-row batches: <= 128 VGPRs
+#ifdef TD3_TL
+    if (threadIdx.x == 0 && blockIdx.x < 8192) td3_tl[blockIdx.x][6] = 1;   // vector tile (tl_probe)
+#endif
+    TL_MARK(3);
+    return;
+  }
+  const int kt = t % P.ntk, nt = t / P.ntk;
+  const int n0 = nt * 64, k0 = kt * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
+  // DMA lanes: wave w fills rows 8w .. 8w+7 of both operands (two 4-row wave-instructions each);
+  // lane L -> row 8w + 4j + L/16, LDS columns 4(L&15) .. +3 <- source columns of the swizzle
+  const int lr = lane >> 4, lc = (lane & 15) * 4;
+  int gcol[2], ucol[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * wave + 4 * j + lr;
+    const int c = lc ^ (((row >> 4) & 1) << 5);
+    gcol[j] = min(n0 + c, P.Np - 4);
+    ucol[j] = min(k0 + c, P.Kp - 4);
+  }
+  auto issue = [&](int st, int buf) {
+    float* g = sm + buf * 2 * 4096;
+    float* u = g + 4096;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rl = 8 * wave + 4 * j;               // first LDS row of this wave-instruction
+      const size_t row = (size_t)(st * 64 + rl + lr);
+      glds16(P.G + row * P.ldg + gcol[j], g + rl * 64);
+      glds16(P.U + row * P.ldu + ucol[j], u + rl * 64);
+    }
+    if constexpr (SC) {
+      if (wave == 0)
+        glds4(P.rs + (size_t)(st * 64 + lane) * P.ldrs, ssl + buf * 64);
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int nstep = a.Bp >> 6;
+  issue(0, 0);
+  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;   // swizzled operand columns of this lane
+  // a quadrant past Np / Kp (the 32-wide edge tiles of a padded 32-multiple) only feeds masked
+  // outputs: its waves keep staging and synchronising but leave the MFMA pipe to a co-resident
+  // workgroup
+  const bool live = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
+  for (int st = 0; st < nstep; ++st) {
+    const int buf = st & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step st has landed
+    __syncthreads();                                 // everyone's has; every wave is done with buffer buf ^ 1
+    if (st + 1 < nstep) issue(st + 1, buf ^ 1);
+    if (!live) continue;
+    const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
+    const float* u = g + 4096;
+    float scl[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * q)
+                           : make_float4(1.f, 1.f, 1.f, 1.f);
+      scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const float ga = g[s2 * 64 + ca];
+      acc = mfma32x32x2(SC ? ga * scl[s2] : ga, u[s2 * 64 + cb], acc);
+    }
+  }
+  __syncthreads();                                   // staging buffers become the reduction tile
+  TL_MARK(1);
+  float* red = sm + (wave & 3) * 32 * 33;
+  if (rh == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[r];
+  }
+  __syncthreads();
   if (rh == 0) {
     const int kk = k0 + qk * 32 + i;
     int64_t idx[16];
@@ -2494,10 +2643,16 @@ int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStr
   return 0;
 }
 
+#ifndef TD3_DW64G
+#define TD3_DW64G 1
+#endif
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s) {
   if (nblocks <= 0) return 0;
   const dim3 grid((nblocks + 7) & ~7);
-  if (a.tile64) {
+  if (a.tile64 && (a.Bp & 63) == 0 && TD3_DW64G) {
+    if (a.scaled) hipLaunchKernelGGL(dw64g_kernel<true>, grid, dim3(512), 0, s, a, nblocks);
+    else hipLaunchKernelGGL(dw64g_kernel<false>, grid, dim3(512), 0, s, a, nblocks);
+  } else if (a.tile64) {
     if (a.scaled) hipLaunchKernelGGL(dw64_kernel<true>, grid, dim3(512), 0, s, a, nblocks);
     else hipLaunchKernelGGL(dw64_kernel<false>, grid, dim3(512), 0, s, a, nblocks);
   } else {

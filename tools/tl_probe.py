@@ -121,6 +121,14 @@ def main():
                 _, cnt = np.unique(cu, return_counts=True)
                 print("   workgroups per CU (histogram 1,2,3..):", np.bincount(cnt).tolist()[1:],
                       " distinct CUs:", len(cnt))
+                if kern.startswith("td3::dw64") and os.environ.get("TL_PAIRS"):
+                    # which dispatch slots (k = blockIdx >> 3 within an XCD) share a CU
+                    bid = np.nonzero(buf[:, 3] != 0)[0]
+                    pairs = {}
+                    for j, c in enumerate(cu.tolist()):
+                        pairs.setdefault(c, []).append((int(bid[j]) >> 3, int(v[j, 6]), round((t3[j] - t0[j]) * 0.01, 1)))
+                    two = [sorted(x) for x in pairs.values() if len(x) == 2]
+                    print("   co-resident slot pairs (k, vector?, dur) sample:", two[:24])
                 q = np.percentile((t1 - t0) * 0.01, [10, 50, 90])
                 print("   end p10/50/90/max:", np.round(np.percentile((t3 - base) * 0.01, [10, 50, 90, 100]), 2).tolist(),
                       " dur p10/50/90/max:", np.round(np.percentile((t3 - t0) * 0.01, [10, 50, 90, 100]), 2).tolist())
