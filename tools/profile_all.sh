@@ -12,3 +12,5 @@ timeout -k 10 400 python3 bench.py --config particles --steps 300 --warmup 20 > 
 echo "particles ok: $(cut -c1-160 gpurun_out/bench_particles_$tag.json)"
 timeout -k 10 300 python3 bench_loop.py > gpurun_out/bench_loop_$tag.json 2> gpurun_out/bench_loop_$tag.err || { echo loop failed; tail gpurun_out/bench_loop_$tag.err; exit 1; }
 echo "loop ok: $(cut -c1-160 gpurun_out/bench_loop_$tag.json)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_humanoid_$tag -o run -- python3 bench.py --config humanoid --steps 300 --warmup 30 --no-cpu-baseline --no-roofline > gpurun_out/prof_humanoid_$tag.log 2>&1 || { echo humanoid trace failed; tail gpurun_out/prof_humanoid_$tag.log; exit 1; }
+echo "humanoid trace ok"
