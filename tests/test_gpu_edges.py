@@ -1,6 +1,8 @@
 """Edge cases of the HIP step against the oracle (teacher-forced, SURVEY.md §8c tolerances).
 
-* ragged batches: B = 1, 33, 257 (row tiles of 32 with 31 / 31 / 31 padding rows);
+* ragged batches: B = 1, 33, 257 (row tiles of 32 with 31 / 31 / 31 padding rows), and the
+  64x64 dW tiles of B >= 512: B = 544 (Bp % 64 = 32: register-staged dw64_kernel) and B = 640
+  (LDS-DMA dw64g_kernel, whose 64-row steps need Bp % 64 = 0; edge tiles with dead quadrants);
 * hidden widths other than the reference's (500, 400, 300) / (500, 400, 200): narrow, odd and
   the 512-wide maximum (every Linear / LayerNorm is padded to 32 in HBM, td3.hip);
 * the widest action space the heads take (32) and the widest network input (512 columns, a
@@ -63,6 +65,12 @@ def _teacher_forced(pol, rb, L, buf, B, ad, seed, steps=2):
 
 @pytest.mark.parametrize("B", [1, 33, 257])
 def test_ragged_batches(B):
+    pol, rb, L, buf = _setup(17, 6)
+    _teacher_forced(pol, rb, L, buf, B, 6, seed=B)
+
+
+@pytest.mark.parametrize("B", [544, 640])
+def test_large_batch_dw_tiles(B):
     pol, rb, L, buf = _setup(17, 6)
     _teacher_forced(pol, rb, L, buf, B, 6, seed=B)
 
