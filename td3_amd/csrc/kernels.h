@@ -56,6 +56,17 @@ enum RowKind : int {
   kRowLnBwd = 9,         // dZ = relu'(LN_bwd(dU)) of full rows (layer 0, no GEMM follows)
 };
 
+// Waves of a single-stage GEMM launch (gemm_kernel): input-grad stages (MODE 1) and 16-column
+// stages (WN = 0) run 16 waves — half the prologue rows per wave (their LN-backward / head
+// prologues are VALU-bound) and twice the K split; the forward LN / fused layer-0 stages and the
+// dual launches (gemm2_kernel) keep kGemmWaves (A/B in DESIGN.md).
+#ifndef TD3_GEMM_NW16
+#define TD3_GEMM_NW16 1
+#endif
+constexpr int gemm_nw(int mode, int wn, int pro) {
+  return (TD3_GEMM_NW16 && pro != kProL0 && pro != kProL0G && (mode == 1 || wn == 0)) ? 16 : kGemmWaves;
+}
+
 constexpr int kMaxEx = 24;
 
 struct GemmProb {

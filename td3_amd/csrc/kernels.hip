@@ -70,16 +70,16 @@ struct Ctx {
   int m0, wave, lane, nt, Bp, S;
 };
 
-template <int RB>
+template <int RPW, int RB = RPW>
 __device__ __forceinline__ void pro_copy(const GemmProb& P, float* smem, const Ctx& c) {
 #pragma unroll
-  for (int r0 = 0; r0 < kRPW; r0 += RB) {
+  for (int r0 = 0; r0 < RPW; r0 += RB) {
     float x[RB][8];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
-      rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r0 + r) * P.lda, P.Kp, c.lane);
+      rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * RPW + r0 + r) * P.lda, P.Kp, c.lane);
 #pragma unroll
-    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * kRPW + r0 + r, P.Kp, c.lane, x[r]);
+    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * RPW + r0 + r, P.Kp, c.lane, x[r]);
   }
 }
 
@@ -87,14 +87,14 @@ struct NoOp {
   __device__ __forceinline__ void operator()() const {}
 };
 
-template <class AfterIssue = NoOp>
+template <int RPW, class AfterIssue = NoOp>
 __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx& c,
                                        const AfterIssue& after_issue = AfterIssue()) {
-  constexpr int RB = kRPW;
+  constexpr int RB = RPW;
   float x[RB][8], g[8], bb[8], mean[RB], rstd[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r)
-    rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r) * P.lda, P.Kp, c.lane);
+    rv_load(x[r], P.A + (size_t)(c.m0 + c.wave * RPW + r) * P.lda, P.Kp, c.lane);
   rv_load(g, P.lng, P.Kp, c.lane);
   rv_load(bb, P.lnb, P.Kp, c.lane);
   after_issue();
@@ -106,7 +106,7 @@ __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx
   const bool t0 = c.nt == 0;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
-    const int row = c.wave * kRPW + r, grow = c.m0 + row;
+    const int row = c.wave * RPW + r, grow = c.m0 + row;
     lds_put_row(smem, c.S, row, P.Kp, c.lane, x[r]);
     if (t0 && P.Aout) rv_store(P.Aout + (size_t)grow * P.ldao, P.Kp, c.lane, x[r]);
     if (t0 && P.stats && c.lane == 0) {
@@ -116,17 +116,18 @@ __device__ __forceinline__ void pro_ln(const GemmProb& P, float* smem, const Ctx
   }
 }
 
+template <int RPW>
 __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const Ctx& c) {
   constexpr int RB = 2;
   float g[8];
   rv_load(g, P.lng, P.Kp, c.lane);
   const bool t0 = c.nt == 0;
 #pragma unroll
-  for (int r0 = 0; r0 < kRPW; r0 += RB) {
+  for (int r0 = 0; r0 < RPW; r0 += RB) {
     float gu[RB][8], h[RB][8], mean[RB], rstd[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const int grow = c.m0 + c.wave * kRPW + r0 + r;
+      const int grow = c.m0 + c.wave * RPW + r0 + r;
       rv_load(gu[r], P.A + (size_t)grow * P.lda, P.Kp, c.lane);
       rv_load(h[r], P.H + (size_t)grow * P.ldh, P.Kp, c.lane);
       mean[r] = P.norm ? gld(P.stats + (grow)) : 0.f;
@@ -136,7 +137,7 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
     else ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.Kreal, c.lane, 0);
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const int row = c.wave * kRPW + r0 + r;
+      const int row = c.wave * RPW + r0 + r;
       lds_put_row(smem, c.S, row, P.Kp, c.lane, gu[r]);
       if (t0 && P.Aout) rv_store(P.Aout + (size_t)(c.m0 + row) * P.ldao, P.Kp, c.lane, gu[r]);
     }
@@ -149,6 +150,7 @@ __device__ __forceinline__ void pro_lnbwd(const GemmProb& P, float* smem, const 
 // alone: LN3 statistics, Q1 = w4 . LN3(H3) + b4 (stored by n-tile 0 for the loss value), then
 // relu'(LN3_bwd(dU3)).  Row work is 3 wave reductions per row on top of pro_lnbwd's 2, so the
 // repetition over column tiles costs less than the row launch it replaces.
+template <int RPW>
 __device__ __forceinline__ void pro_headbwd(const GemmProb& P, float* smem, const Ctx& c) {
   constexpr int RB = 2;
   float g[8], w[8], rm[8], bb[8];
@@ -161,11 +163,11 @@ __device__ __forceinline__ void pro_headbwd(const GemmProb& P, float* smem, cons
   real_mask(rm, P.Kreal, c.lane);
   const float invK = 1.0f / (float)P.Kreal;
   const bool t0 = c.nt == 0;
-  float hall[kRPW][8];          // all of the wave's rows in one load round
+  float hall[RPW][8];          // all of the wave's rows in one load round
 #pragma unroll
-  for (int r = 0; r < kRPW; ++r) rv_load(hall[r], P.A + (size_t)(c.m0 + c.wave * kRPW + r) * P.lda, P.Kp, c.lane);
+  for (int r = 0; r < RPW; ++r) rv_load(hall[r], P.A + (size_t)(c.m0 + c.wave * RPW + r) * P.lda, P.Kp, c.lane);
 #pragma unroll
-  for (int r0 = 0; r0 < kRPW; r0 += RB) {
+  for (int r0 = 0; r0 < RPW; r0 += RB) {
     float h[RB][8], gu[RB][8], mean[RB], rstd[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
@@ -198,19 +200,19 @@ __device__ __forceinline__ void pro_headbwd(const GemmProb& P, float* smem, cons
         for (int j = 0; j < 8; ++j)
           x[r][j] = P.norm ? __fmaf_rn(__fmaf_rn(h[r][j], rstd[r], nb), g[j], bb[j]) : h[r][j];
         const float q = wsum(rv_pdot(x[r], w, P.Kreal, c.lane)) + b4;
-        if (c.lane == 0) gst(P.ex[5] + (c.m0 + c.wave * kRPW + r0 + r), q);
+        if (c.lane == 0) gst(P.ex[5] + (c.m0 + c.wave * RPW + r0 + r), q);
       }
     }
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const float gq = c.m0 + c.wave * kRPW + r0 + r < P.B ? P.exf[0] : 0.f;
+      const float gq = c.m0 + c.wave * RPW + r0 + r < P.B ? P.exf[0] : 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) gu[r][j] = gq * w[j];
     }
     if (P.norm) ln_bwd_rows_pk<RB>(gu, h, g, mean, rstd, invK);
     else ln_bwd_rows<RB>(gu, h, g, mean, rstd, P.Kreal, c.lane, 0);
 #pragma unroll
-    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * kRPW + r0 + r, P.Kp, c.lane, gu[r]);
+    for (int r = 0; r < RB; ++r) lds_put_row(smem, c.S, c.wave * RPW + r0 + r, P.Kp, c.lane, gu[r]);
   }
 }
 
@@ -240,20 +242,21 @@ __device__ __forceinline__ float* rw_ptr(const GemmProb& P, int lane) {
   asm volatile("" : "+s"(r0), "+s"(r1));   // pinned in SGPRs: the select below is a v_cndmask
   return lane == 0 ? r0 : r1;
 }
+template <int RPW>
 __device__ __forceinline__ void pro_gather(const GemmProb& P, const RingSide& rs, float* smem, const Ctx& c,
                                            int pi) {
   const uint64_t step = (uint64_t)(rs.ctr->total_it + 1);
   const uint64_t n = (uint64_t)*rs.d_size;
-  int64_t idx[kRPW];
+  int64_t idx[RPW];
 #pragma unroll
-  for (int r = 0; r < kRPW; ++r) {
-    const int grow = c.m0 + c.wave * kRPW + r;
+  for (int r = 0; r < RPW; ++r) {
+    const int grow = c.m0 + c.wave * RPW + r;
     idx[r] = grow < P.B ? (int64_t)philox_index(rs.seed, step, (uint32_t)grow, n) : -1;
   }
   const bool t0 = c.nt == 0;
-  float x[kRPW][8], rw[kRPW];
+  float x[RPW][8], rw[RPW];
 #pragma unroll
-  for (int r = 0; r < kRPW; ++r) {
+  for (int r = 0; r < RPW; ++r) {
     rw[r] = 0.f;
     if (idx[r] >= 0) {
       const float* rec = rs.data + (size_t)idx[r] * rs.rec;
@@ -265,11 +268,11 @@ __device__ __forceinline__ void pro_gather(const GemmProb& P, const RingSide& rs
     }
   }
 #pragma unroll
-  for (int r = 0; r < kRPW; ++r) lds_put_row(smem, c.S, c.wave * kRPW + r, P.Kp, c.lane, x[r]);
+  for (int r = 0; r < RPW; ++r) lds_put_row(smem, c.S, c.wave * RPW + r, P.Kp, c.lane, x[r]);
   if (!t0) return;
 #pragma unroll
-  for (int r = 0; r < kRPW; ++r) {
-    const int grow = c.m0 + c.wave * kRPW + r;
+  for (int r = 0; r < RPW; ++r) {
+    const int grow = c.m0 + c.wave * RPW + r;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int col = rcol(c.lane, j);
@@ -1178,15 +1181,17 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 #define TD3_L0_LATE_B 0
 #endif
 // One workgroup's tile b of a GEMM stage (the body of gemm_kernel / gemm2_kernel).
-template <int MODE, int WN, int PRO>
+template <int MODE, int WN, int PRO, int NW = kNW>
 __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, int tb3, int Bp, const GemmTable& tab,
                                           Counters* bump, int bump_actor, float* smem) {
+  constexpr int RPW = 32 / NW;                 // prologue rows per wave
+  static_assert(NW == kNW || (PRO != kProL0 && PRO != kProL0G), "fused layer 0 runs kNW waves");
   // WN = 0: 16 output columns per workgroup on v_mfma_f32_16x16x4_f32 (two 16-row halves of the
   // 32-row tile): half the MFMA chain of WN = 1 for stages of <= 128 32-column workgroups, which
   // otherwise leave half the CUs idle (td3.hip gemm_wn)
   constexpr int WNS = WN == 0 ? 1 : WN;        // waves per K group
-  constexpr int WK = kNW / WNS;
-  constexpr int NT = 64 * kNW;                 // threads
+  constexpr int WK = NW / WNS;
+  constexpr int NT = 64 * NW;                  // threads
   constexpr int OUTW = WN == 0 ? 16 : 32 * WN; // output columns of the workgroup
   constexpr bool kPrefetchB = true;
   int pi = 0;
@@ -1247,7 +1252,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
 
   // weight chunks requested at the kernel start (the rest stream in the MFMA loop).  Prefetching
   // all 4 chunks of a WN=2 wave was no faster: the A-row loads then queue behind 16 weight loads.
-  constexpr int kCh = kMaxChunks;
+  constexpr int kCh = 16 / NW;                // weight chunks a wave requests up front
   float bv[kCh][16];
   // bias of the epilogue's column, requested with the weights (off the tail of the chain)
   const int bcol = (WK == 1) ? ncol : n0 + (int)(threadIdx.x % OUTW);
@@ -1306,11 +1311,11 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
     }
   };
 
-  if constexpr (PRO == kProCopy) pro_copy<kRPW>(P, smem, c);
-  else if constexpr (PRO == kProLN) pro_ln(P, smem, c, issue_stream);
-  else if constexpr (PRO == kProLNBwd) pro_lnbwd(P, smem, c);
-  else if constexpr (PRO == kProHeadBwd) pro_headbwd(P, smem, c);
-  else if constexpr (PRO == kProGather) pro_gather(P, tab.rs, smem, c, pi);
+  if constexpr (PRO == kProCopy) pro_copy<RPW>(P, smem, c);
+  else if constexpr (PRO == kProLN) pro_ln<RPW>(P, smem, c, issue_stream);
+  else if constexpr (PRO == kProLNBwd) pro_lnbwd<RPW>(P, smem, c);
+  else if constexpr (PRO == kProHeadBwd) pro_headbwd<RPW>(P, smem, c);
+  else if constexpr (PRO == kProGather) pro_gather<RPW>(P, tab.rs, smem, c, pi);
   else if constexpr (kL0) {
     float* xs = smem + 32 * S;
     l0_put_x<PRO == kProL0G>(P, tab.rs, xs, c, pi, l0x);
@@ -1428,7 +1433,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
     TL_MARK(2);
   } else {
     __syncthreads();
-    float* red = smem;  // [kNW][32][33]; wave = wk * WNS + wn
+    float* red = smem;  // [NW][32][33]; wave = wk * WNS + wn
     if constexpr (WN == 0) {
       // 16x16 C/D map: column lane & 15, row 4 * (lane >> 4) + j
 #pragma unroll
@@ -1442,9 +1447,11 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
     }
     __syncthreads();
     TL_MARK(2);
+    // (32 x OUTW outputs over NT threads: 16 waves of a 16-column tile leave half the threads idle)
 #pragma unroll
-    for (int q = 0; q < 32 * OUTW / NT; ++q) {
+    for (int q = 0; q < (32 * OUTW + NT - 1) / NT; ++q) {
       const int e = threadIdx.x + NT * q;
+      if (32 * OUTW % NT != 0 && e >= 32 * OUTW) break;
       const int row = e / OUTW, colw = e % OUTW;
       const int wnn = colw >> 5, ci = colw & 31;
       float v = red[(wnn * 32 + row) * 33 + ci];
@@ -1472,13 +1479,14 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
 }
 
 template <int MODE, int WN, int PRO>
-__global__ __launch_bounds__(64 * kNW, WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
+__global__ __launch_bounds__(64 * gemm_nw(MODE, WN, PRO), WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
                                                         GemmTable tab, Counters* bump, int bump_actor) {
   extern __shared__ float4 smem4[];
   const int b = xcd_tile(nb);
   TL_MARK(0);
   if (b >= nb) return;
-  gemm_body<MODE, WN, PRO>(b, nprob, tb1, tb2, tb3, Bp, tab, bump, bump_actor, reinterpret_cast<float*>(smem4));
+  gemm_body<MODE, WN, PRO, gemm_nw(MODE, WN, PRO)>(b, nprob, tb1, tb2, tb3, Bp, tab, bump, bump_actor,
+                                                   reinterpret_cast<float*>(smem4));
 }
 
 // Two independent GEMM stages in one launch (the unit-gradient critic backward beside the target
@@ -2429,7 +2437,9 @@ static void gl(const GemmTable& t, int nblocks, int Bp, int lds, Counters* bump,
   const int padded = (nblocks + 7) & ~7;
   const int tb1 = t.nprob > 1 ? t.p[1].tile_begin : nblocks, tb2 = t.nprob > 2 ? t.p[2].tile_begin : nblocks;
   const int tb3 = t.nprob > 3 ? t.p[3].tile_begin : nblocks;
-  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(64 * kNW), lds, s, nblocks, t.nprob, tb1,
+  constexpr int nw = gemm_nw(MODE, WN, PRO);
+  const int l = std::max(lds, nw * 32 * 33 * 4);   // the K-split reduction tile of nw waves
+  hipLaunchKernelGGL((gemm_kernel<MODE, WN, PRO>), dim3(padded), dim3(64 * nw), l, s, nblocks, t.nprob, tb1,
                      tb2, tb3, Bp, t, bump, ba);
 }
 
