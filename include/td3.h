@@ -99,7 +99,11 @@ int rb_sample_particles(rb_handle* h, int batch, float* feat, float* part, float
                         int64_t* idx_out, void* stream);
 
 /* ------------------------------------------------------------------ learner */
+/* struct_size: sizeof(td3_config) as the caller compiled it.  td3_default_config sets it and
+ * td3_create refuses a config whose struct_size differs from the library's (a binding written
+ * against another version of this header), before reading any other field. */
 typedef struct td3_config {
+  int struct_size;
   int state_dim, action_dim;
   int actor_hidden[3];     /* reference: (500, 400, 300)  TD3_featured.py:19 */
   int critic_hidden[3];    /* reference: (500, 400, 200)  TD3_featured.py:54 */
@@ -136,7 +140,11 @@ typedef struct td3_step_stats {   /* particles: y / q1 / q2 are [B][action_dim] 
   float* noise;            /* nullable host [B][ad]: the N(0,1) draw of randn_like (:132) */
 } td3_step_stats;
 
-void td3_default_config(td3_config* cfg);
+/* sizeof(td3_config) of this library: a binding checks its own struct against it. */
+size_t td3_config_size(void);
+/* Reference defaults (TD3_base.py:7-24, TD3_featured.py:100, main.py:112-126).  cfg_size is the
+ * caller's sizeof(td3_config): on a mismatch nothing is written and -1 is returned. */
+int td3_default_config(td3_config* cfg, size_t cfg_size);
 int td3_create(const td3_config* cfg, td3_handle** out);
 int td3_destroy(td3_handle* h);
 

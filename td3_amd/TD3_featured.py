@@ -207,8 +207,7 @@ class TD3(TD3_base):
         self._dev = default_device_index() if device is None else int(device)
         torch = _torch()
         self.device = torch.device("cuda", self._dev)
-        cfg = _lib.td3_config()
-        self._lib.td3_default_config(C.byref(cfg))
+        cfg = _lib.default_config()
         cfg.state_dim, cfg.action_dim = sd, ad
         for i in range(3):
             cfg.actor_hidden[i] = actor_arch[i]

@@ -96,8 +96,7 @@ class TD3(_FeaturedTD3):
         self._dev = default_device_index() if device is None else int(device)
         torch = _torch()
         self.device = torch.device("cuda", self._dev)
-        cfg = _lib.td3_config()
-        self._lib.td3_default_config(C.byref(cfg))
+        cfg = _lib.default_config()
         cfg.state_dim, cfg.action_dim = F, A
         for i in range(3):
             cfg.actor_hidden[i] = ARCH[i]

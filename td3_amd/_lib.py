@@ -22,7 +22,7 @@ class rb_info_t(C.Structure):
 
 
 class td3_config(C.Structure):
-    _fields_ = [("state_dim", C.c_int), ("action_dim", C.c_int),
+    _fields_ = [("struct_size", C.c_int), ("state_dim", C.c_int), ("action_dim", C.c_int),
                 ("actor_hidden", C.c_int * 3), ("critic_hidden", C.c_int * 3),
                 ("norm", C.c_int), ("max_action", C.c_float),
                 ("discount", C.c_double), ("tau", C.c_double), ("policy_noise", C.c_double),
@@ -61,7 +61,8 @@ SIGNATURES = {
                                       C.POINTER(_P)]),
     "rb_add_particles": (C.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, C.c_int64, _P]),
     "rb_sample_particles": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "td3_default_config": (None, [C.POINTER(td3_config)]),
+    "td3_config_size": (C.c_size_t, []),
+    "td3_default_config": (C.c_int, [C.POINTER(td3_config), C.c_size_t]),
     "td3_create": (C.c_int, [C.POINTER(td3_config), C.POINTER(_P)]),
     "td3_destroy": (C.c_int, [_P]),
     "td3_tensor_count": (C.c_int, [_P, C.c_int]),
@@ -146,6 +147,18 @@ def check(rc: int, what: str = ""):
     if rc != 0:
         msg = _lib.td3_last_error().decode(errors="replace") if _lib is not None else ""
         raise TD3Error(f"{what} failed ({rc}): {msg}")
+
+
+def default_config():
+    """A td3_config filled with the library's defaults (TD3_base / TD3_featured hyper-parameters);
+    raises when this binding's struct layout differs from the library's include/td3.h."""
+    lib = load()
+    if C.sizeof(td3_config) != lib.td3_config_size():
+        raise TD3Error(f"td3_config binding is {C.sizeof(td3_config)} bytes, libtd3hip's "
+                       f"{lib.td3_config_size()}: td3_amd/_lib.py is out of date with include/td3.h")
+    cfg = td3_config()
+    check(lib.td3_default_config(C.byref(cfg), C.sizeof(cfg)), "td3_default_config")
+    return cfg
 
 
 def fptr(a):

@@ -2086,8 +2086,17 @@ extern "C" {
 
 const char* td3_last_error(void) { return g_err; }
 
-void td3_default_config(td3_config* c) {
+size_t td3_config_size(void) { return sizeof(td3_config); }
+
+int td3_default_config(td3_config* c, size_t cfg_size) {
+  TD3_ARG(c != nullptr, "null config");
+  if (cfg_size != sizeof(td3_config)) {
+    set_error("td3_default_config: caller's td3_config is %zu bytes, the library's %zu (binding out of date "
+              "with include/td3.h)", cfg_size, sizeof(td3_config));
+    return -1;
+  }
   memset(c, 0, sizeof(*c));
+  c->struct_size = (int)sizeof(td3_config);
   c->actor_hidden[0] = 500; c->actor_hidden[1] = 400; c->actor_hidden[2] = 300;    // TD3_featured.py:19
   c->critic_hidden[0] = 500; c->critic_hidden[1] = 400; c->critic_hidden[2] = 200; // TD3_featured.py:54
   c->norm = 1;
@@ -2106,6 +2115,7 @@ void td3_default_config(td3_config* c) {
   c->use_graph = 2;
   c->particles = 0;
   c->cdq = 1;
+  return 0;
 }
 
 // Device counters with the Adam bias-correction powers at these steps (Python's beta ** step).
@@ -2127,6 +2137,11 @@ static Counters make_counters(const td3_handle* h, int64_t total_it, int64_t cri
 
 int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_ARG(cfg && out, "null argument");
+  if (cfg->struct_size != (int)sizeof(td3_config)) {
+    set_error("td3_create: td3_config.struct_size is %d, the library's td3_config is %zu bytes (fill it with "
+              "td3_default_config; binding out of date with include/td3.h?)", cfg->struct_size, sizeof(td3_config));
+    return -1;
+  }
   TD3_ARG(cfg->state_dim > 0 && cfg->action_dim > 0, "dims must be positive");
   TD3_ARG(cfg->action_dim <= 32, "action_dim > 32 not supported by the head kernels");
   TD3_ARG(cfg->policy_freq > 0, "policy_freq must be positive");
