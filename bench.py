@@ -13,8 +13,10 @@ rows; gradients are all-reduced over RCCL (xGMI) before Adam.  ``value`` counts
 batch-256 gradient steps over all ranks (weak scaling).
 
 Prints ONE JSON line on rank 0 (the driver contract) with a ``roofline`` object for the
-dominant kernel (HIP-event timed live) and a ``cpu_baseline`` (the numpy oracle on the
-host cores, rank 0, N=1 only).
+dominant kernel (HIP-event timed live; ``step_frac`` = the step's algorithmic FLOP / measured
+step time / fp32 MFMA peak), a ``gather`` object for the replay-ring sample kernel (bytes / HIP
+event time vs the 8 TB/s HBM peak) and a ``cpu_baseline`` (the torch-CPU restatement of the
+reference step, oracle/td3_torch_cpu.py, on the host cores of this box: rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -49,6 +51,9 @@ CONFIGS = {
                                "LayerNorm, CDQ, policy_freq 2, replay 1e5 per GPU"),
 }
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8 TB/s spec
+# per-config rocprofv3 PMC summaries (tools/pmc_summary.py output): HBM bytes per launch per kernel
+PMC_FILES = {"halfcheetah": "pmc_traffic.json", "humanoid": "pmc_traffic_humanoid.json",
+             "particles": "pmc_traffic_particles.json"}
 FP32_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: f32 MFMA / vector peak
 
 
@@ -87,6 +92,73 @@ def stage_table(pol, rb, batch, iters=50, reps=5):
     return rows
 
 
+def step_flops(cfg):
+    """Algorithmic FLOP of one gradient step, the mean of a critic-only and a policy step (SURVEY.md
+    §8d): per sample, critic phase = target actor fwd + target twin fwd + twin fwd + twin dW + twin
+    dX (no input layer), actor phase = actor fwd + dW + dX (no input layer) + Q1 fwd + dX; MACs of a
+    network = sum of in*out over its Linears.  Particles add the per-particle encoder (conv1 1xD,
+    conv2 1x1 over N particles: fwd E, bwd E + N*256*128 for dh1; no encoder grad for Q1 in the
+    actor phase).  C2 1.753 GFLOP, C3 10.416 GFLOP, C4 1126 GFLOP."""
+    B, ad = cfg["batch"], cfg["ad"]
+    def mlp(inp, arch, out):
+        dims = [inp] + list(arch) + [out]
+        return sum(a * b for a, b in zip(dims[:-1], dims[1:])), dims[0] * dims[1]
+    if cfg["kind"] == "particles":
+        F, N, D = cfg["F"], cfg["N"], cfg["D"]
+        Af, _ = mlp(128 + F, (500, 400, 300), ad)
+        Qf, _ = mlp(128 + F + ad, (500, 400, 300), ad)
+        E = N * (256 * D + 128 * 256)
+        Eb = E + N * 256 * 128
+        critic = (E + Af) + 4 * (E + Qf) + 4 * Qf + 2 * Eb
+        actor = (E + Af) + (E + Qf) + Qf + 2 * Af + Eb
+    else:
+        sd = cfg["sd"]
+        Af, Ain = mlp(sd, (500, 400, 300), ad)
+        Qf, Qin = mlp(sd + ad, (500, 400, 200), 1)
+        critic = Af + 6 * Qf + 2 * (Qf - Qin)
+        actor = 3 * Af - Ain + 2 * Qf
+    return 2.0 * B * (critic + actor / 2.0)
+
+
+def gather_line(pol, rb, cfg, reps=5, iters=40):
+    """The replay-ring sample (gather_kernel: Philox draw, record reads, batch-row writes) timed on
+    its own from a captured graph (td3_time_stage stage 0), against the HBM peak.  Bytes: the
+    sampled records read whole (featured: rec = pad4(2 sd + ad + 2) floats; particle rings read only
+    the small fields, the encoders read the particle blocks in place) and the batch rows written
+    (td3.hip input_from_ring*: featured [s | a], s, s', r, not_done; padded rows are written too)."""
+    lib, h = pol._lib, pol._h
+    B = cfg["batch"]
+    Bp = (B + 31) // 32 * 32
+    ad = cfg["ad"]
+    if cfg["kind"] == "particles":
+        F = cfg["F"]
+        per_row = 3 * F + 2 * (2 * F + ad) + 2          # XA, XAQ, XTA, XQ_j [f | a], XTQ_j, r, nd (CDQ)
+        read, written = B * per_row * 4, Bp * per_row * 4
+        algorithmic = B * 4 * (2 * (F + cfg["N"] * cfg["D"]) + ad + 2)
+    else:
+        sd = cfg["sd"]
+        rec = (2 * sd + ad + 2 + 3) // 4 * 4
+        read, written = B * rec * 4, Bp * (3 * sd + ad + 2) * 4
+        algorithmic = B * 4 * (2 * sd + ad + 2)
+    t = C.c_float()
+    runs = []
+    for _ in range(reps):
+        rc = lib.td3_time_stage(h, 0, iters, C.byref(t))
+        if rc:
+            raise RuntimeError(lib.td3_last_error().decode())
+        runs.append(float(t.value))
+    us = float(np.median(runs)) * 1e3
+    moved = read + written
+    return {"kernel": "td3::gather_kernel", "bound": "hbm", "us": round(us, 3),
+            "bytes_read": int(read), "bytes_written": int(written),
+            "achieved": round(moved / us * 1e-3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(moved / us * 1e-3 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes": int(2 * algorithmic),
+            "algorithmic_TBps": round(2 * algorithmic / us * 1e-6, 3),
+            "in_step": "separate launch" if cfg["kind"] == "particles" or cfg["sd"] * 2 + ad + 2 > 128
+                       else "fused into F_fwd01 (kProL0G); this line is the stand-alone kernel"}
+
+
 def roofline_from_stages(rows, pmc):
     """Dominant kernel over one odd + one even step; achieved = algorithmic FLOP / time."""
     fam = {}
@@ -110,17 +182,33 @@ def roofline_from_stages(rows, pmc):
             "flops_per_launch": per_launch_flops}, fam
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg, seconds=12.0):
-    """The numpy oracle (oracle/td3_oracle.py, a restatement of TD3_*.train pinned to the
-    reference's goldens) on this host's cores: same shapes and batch as the GPU line."""
+    """The reference's CPU path restated in torch (oracle/td3_torch_cpu.py: F.linear / F.layer_norm
+    forward, autograd, torch.optim.Adam, pinned to the reference's goldens by
+    tests/test_torch_cpu_restatement.py) on this host's cores: same shapes and batch as the GPU
+    line.  Threads: every CPU this process may run on (os.sched_getaffinity), capped by
+    OMP_NUM_THREADS when set (the GPU box gives a job 16 CPUs of a larger machine)."""
+    import torch
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import gen
     from oracle import td3_oracle as orc
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
-    except Exception:
-        cores = os.cpu_count() or 1
+    from oracle.td3_torch_cpu import FeaturedTorch, ParticleTorch
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
     B, ad = cfg["batch"], cfg["ad"]
     rs = np.random.RandomState(0)
     rows = 2048 if cfg["kind"] == "particles" else 20000
@@ -128,37 +216,42 @@ def cpu_baseline(cfg, seconds=12.0):
         F, N, D = cfg["F"], cfg["N"], cfg["D"]
         a0 = gen.init_params(gen.particle_actor_shapes(F, D, ad, "layer"), 1)
         c0 = gen.init_params(gen.particle_critic_shapes(F, D, ad, "layer"), 2)
-        L = orc.Learner(a0, c0, norm="layer")
+        L = ParticleTorch(a0, c0, norm="layer")
         buf = orc.ParticleBuffer(F, N, D, ad, rows)
         buf.state_features[:] = rs.standard_normal(buf.state_features.shape)
         buf.state_particles[:] = rs.standard_normal(buf.state_particles.shape)
         buf.next_state_features[:] = rs.standard_normal(buf.next_state_features.shape)
         buf.next_state_particles[:] = rs.standard_normal(buf.next_state_particles.shape)
-        step, what = orc.particle_train_step, "particles F7 N350 D9 A3"
+        what = "particles F7 N350 D9 A3"
     else:
         sd = cfg["sd"]
         a0 = gen.init_params(gen.featured_actor_shapes(sd, ad, "layer"), 1)
         c0 = gen.init_params(gen.featured_critic_shapes(sd, ad, "layer"), 2)
-        L = orc.Learner(a0, c0, max_action=cfg["ma"], norm="layer")
+        L = FeaturedTorch(a0, c0, max_action=cfg["ma"], norm="layer")
         buf = orc.FeaturedBuffer(sd, ad, rows)
         buf.state[:] = rs.standard_normal((rows, sd))
         buf.next_state[:] = rs.standard_normal((rows, sd))
-        step, what = orc.featured_train_step, f"state {sd} action {ad}"
+        what = f"state {sd} action {ad}"
     buf.action[:] = rs.uniform(-cfg["ma"], cfg["ma"], buf.action.shape)
     buf.reward[:] = rs.standard_normal((rows, 1))
     buf.not_done[:] = (rs.uniform(size=(rows, 1)) > 0.01)
     buf.size = rows
+    if cfg["kind"] != "particles":          # one untimed step (allocator / thread-pool warm-up)
+        L.train_step(buf.gather(rs.randint(0, rows, B)), rs.standard_normal((B, ad)).astype(np.float32))
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds or steps < 2:
         idx = rs.randint(0, rows, B)
         noise = rs.standard_normal((B, ad)).astype(np.float32)
-        step(L, buf.gather(idx), noise)
+        L.train_step(buf.gather(idx), noise)
         steps += 1
     dt = time.perf_counter() - t0
+    torch.set_num_threads(prev)
     return {"value": round(steps / dt, 4), "unit": "grad-steps/s", "cores": int(cores),
-            "kind": "port",
-            "sample": f"{steps} oracle train steps ({what}, B={B}, norm=layer) in {dt:.1f} s"}
+            "kind": "port", "cpu_model": _cpu_model(),
+            "implementation": "oracle/td3_torch_cpu.py (torch-CPU restatement of TD3.train, "
+                              f"torch {torch.__version__}, {cores} threads)",
+            "sample": f"{steps} torch-CPU train steps ({what}, B={B}, norm=layer, warm) in {dt:.1f} s"}
 
 
 def main():
@@ -210,14 +303,8 @@ def main():
     rb = RB(obs, Box((cfg["ad"],)), max_size=REPLAY_ROWS, device=local, seed=101 + rank)
     rb.fill_synthetic(REPLAY_ROWS, cfg["ma"], seed=7 + rank)
     if world > 1:
-        uid = (C.c_ubyte * 128)()
-        t = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            _lib.check(pol._lib.td3_comm_unique_id(uid), "td3_comm_unique_id")
-            t.copy_(torch.tensor(list(bytes(uid)), dtype=torch.uint8))
-        dist.broadcast(t, 0)
-        uid = (C.c_ubyte * 128)(*t.cpu().tolist())
-        _lib.check(pol._lib.td3_comm_init(pol._h, uid, world, rank), "td3_comm_init")
+        from td3_amd.data_parallel import init_rccl
+        init_rccl(pol, dist)
 
     def barrier_sync():
         pol.sync()
@@ -242,17 +329,22 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    rows, fam, roof = None, None, None
+    rows, fam, roof, gat = None, None, None, None
     if not args.no_roofline:           # every rank runs it: profiled steps contain collectives
         rows = stage_table(pol, rb, B, iters=50 if cfg["kind"] != "particles" else 3,
                            reps=5 if cfg["kind"] != "particles" else 1)
+        gat = gather_line(pol, rb, cfg)
         if rank == 0:
             pmc = None
-            pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc_path) and args.config == "halfcheetah":
+            pmc_path = os.path.join(ROOT, "profiles", PMC_FILES.get(args.config, ""))
+            if os.path.isfile(pmc_path) and args.norm == "layer":
                 with open(pmc_path) as f:
                     pmc = json.load(f)
             roof, fam = roofline_from_stages(rows, pmc)
+            if roof.get("traffic") is not None:
+                roof["traffic_source"] = (f"profiles/{PMC_FILES[args.config]}: rocprofv3 --pmc FETCH_SIZE / "
+                                          "WRITE_SIZE of this kernel in a separate profiling run of this "
+                                          "configuration (committed; not measured inside this run)")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -286,7 +378,12 @@ def main():
                        "launch": args.launch, "norm": args.norm},
         }
         if roof is not None:
+            flops = step_flops(cfg)
+            roof["step_flops"] = flops
+            roof["step_frac"] = round(flops / (dt / args.steps) / (FP32_PEAK_TFLOPS * 1e12), 4)
             out["roofline"] = roof
+        if gat is not None:
+            out["gather"] = gat
             out["stage_us"] = {f"{r['phase']}:{r['stage']}": round(r["ms"] * 1e3, 2) for r in rows}
         if cpu is not None:
             out["cpu_baseline"] = cpu

@@ -20,6 +20,8 @@
  *   td3_select_action    TD3.select_action                TD3_featured.py:113-115
  *   td3_eval_q           TD3.eval_q                       TD3_featured.py:117-121
  *   td3_*_particles      TD3_particles.TD3 (set encoder)  TD3_particles.py:136-224
+ *   td3_actor_learn_particles TD3_particles.TD3._actor_learn TD3_particles.py:209-224
+ *   td3_comm_init(_local) data-parallel extension (the reference is single-device)
  *
  * Ownership: handles own all device memory.  Host pointers are owned by the caller
  * and only read/written during the call.  Device pointers passed in (rb_sample
@@ -185,6 +187,13 @@ int td3_train_step_batch_particles(td3_handle* h, const float* feat, const float
                                    const float* next_feat, const float* next_part, const float* reward,
                                    const float* not_done, int batch, void* stream, const float* inject_noise,
                                    td3_step_stats* stats);
+/* TD3_particles.TD3._actor_learn(state_features, state_particles) (TD3_particles.py:209-224), as
+ * evaluate_model.py:39-49 calls it outside train(): -mean Q1(s, pi(s)) with the current critic, the
+ * actor's Adam step (its step counter only; total_it unchanged), Polyak of critic and actor.
+ * feat [batch][F] / part [batch][N][D]: device float32, contiguous.  actor_loss (nullable, forces a
+ * sync) receives the loss value. */
+int td3_actor_learn_particles(td3_handle* h, const float* feat, const float* part, int batch, void* stream,
+                              double* actor_loss);
 /* host feat [n][F], part [n][N][D] -> action_out [n][A] (tanh policy) */
 int td3_select_action_particles(td3_handle* h, const float* feat, const float* part, float* action_out, int n);
 /* -> q_out [2][n][A] (Q1, then Q2; Q2 = Q1 when CDQ is off) */
@@ -195,6 +204,17 @@ int td3_eval_q_particles(td3_handle* h, const float* feat, const float* part, co
 int td3_comm_unique_id(unsigned char out[128]);
 /* Data-parallel mode: grads are all-reduced (sum, then /world) over RCCL before Adam. */
 int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int rank);
+/* Test seam of the same data-parallel path inside ONE process (RCCL cannot put two ranks on one
+ * GPU): the n handles (same configuration and device) become the ranks 0..n-1 of a group whose
+ * all-reduce is a fixed-order device sum over their G arenas.  Their plans switch to the
+ * data-parallel stage lists exactly as td3_comm_init does (grad-only dW, all-reduce, flat Adam with
+ * grad_scale 1/n, Polyak); they step together through td3_train_step_local only. */
+int td3_comm_init_local(td3_handle** hs, int n);
+/* One TD3.train step of every replica of a td3_comm_init_local group, stage by stage on rank 0's
+ * stream; replica k samples rbs[k].  inject_idx [n][batch] / inject_noise [n][batch][ad] (host,
+ * nullable) as td3_train_step; stats [n] (nullable). */
+int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, const int64_t* inject_idx,
+                         const float* inject_noise, td3_step_stats* stats);
 
 /* ------------------------------------------------------------------ measurement */
 int td3_sync(td3_handle* h);
@@ -207,7 +227,7 @@ const char* td3_stage_name(td3_handle* h, int i);
 const char* td3_stage_kernel(td3_handle* h, int i);
 /* Re-launch one stage `iters` times back-to-back (captured in one hipGraph, replayed between
  * two HIP events on the handle stream, after one full step at `batch`); returns mean ms per
- * launch. */
+ * launch.  Stage 0 is the stand-alone replay-ring gather (gather_kernel) of the profiled ring. */
 int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean);
 /* Algorithmic FLOPs of one launch of stage i (MFMA stages; 0 otherwise). */
 double td3_stage_flops(td3_handle* h, int i);

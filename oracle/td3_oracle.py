@@ -456,18 +456,27 @@ def particle_train_step(L: Learner, batch, noise, record=None):
     rec["critic_grads"] = grads
     L.adam_critic(grads)
     if L.total_it % L.policy_freq == 0:                                     # :206-207
-        pi, ac = particle_net(L.actor, "", L.norm, f, p, actor=True)         # :211
-        aq1, qc = particle_net(L.critic, "q1.", L.norm, f, p, pi)          # :212
-        rec.update(pi=pi, actor_q1=aq1, actor_loss=-float(np.mean(aq1, dtype=np.float64)))
-        gq = np.full(aq1.shape, -1.0 / aq1.size, dtype=f32)
-        _, gx = particle_net_backward(L.norm, "q1.", qc, gq)
-        Fd = f.shape[1]
-        gpi = gx[:, 128 + Fd:]
-        ag, _ = particle_net_backward(L.norm, "", ac, gpi, actor=True)
-        ag = _ordered(ag, L.actor)
-        rec["actor_grads"] = ag
-        L.adam_actor(ag)
-        L.polyak()                                                          # :219-224
+        particle_actor_learn(L, f, p, rec)
+    return rec
+
+
+def particle_actor_learn(L: Learner, f, p, record=None):
+    """``TD3_particles.TD3._actor_learn(state_features, state_particles)`` (TD3_particles.py:209-224):
+    actor loss -mean Q1(s, pi(s)), the actor's Adam step, then Polyak of critic and actor.  It is
+    also called on its own (evaluate_model.py:39-49); ``total_it`` is not touched."""
+    rec = record if record is not None else {}
+    pi, ac = particle_net(L.actor, "", L.norm, f, p, actor=True)             # :211
+    aq1, qc = particle_net(L.critic, "q1.", L.norm, f, p, pi)              # :212
+    rec.update(pi=pi, actor_q1=aq1, actor_loss=-float(np.mean(aq1, dtype=np.float64)))
+    gq = np.full(aq1.shape, -1.0 / aq1.size, dtype=f32)
+    _, gx = particle_net_backward(L.norm, "q1.", qc, gq)
+    Fd = f.shape[1]
+    gpi = gx[:, 128 + Fd:]
+    ag, _ = particle_net_backward(L.norm, "", ac, gpi, actor=True)
+    ag = _ordered(ag, L.actor)
+    rec["actor_grads"] = ag
+    L.adam_actor(ag)                                                        # :215-217
+    L.polyak()                                                              # :219-224
     return rec
 
 

@@ -170,6 +170,24 @@ class TD3(_FeaturedTD3):
                                              _lib.fptr(q), 1), "td3_eval_q_particles")
         return [q[0].copy(), q[1].copy()] if self.CDQ else [q[0].copy()]
 
+    def _actor_learn(self, state_features, state_particles, stats=False):
+        """TD3_particles.py:209-224: the delayed policy update on the given states (torch tensors or
+        arrays, [B, F] and [B, N, D]), as ``evaluate_model.py:39-49`` calls it outside ``train``:
+        -mean Q1(s, pi(s)), the actor's Adam step, Polyak of critic and actor.  ``total_it`` is not
+        touched.  Returns None like the reference (``stats=True``: the actor loss)."""
+        torch = _torch()
+        F, N, D = self.feat_dim, self.n_particles, self.particle_dim
+        f = torch.as_tensor(state_features, dtype=torch.float32).to(self.device).reshape(-1, F).contiguous()
+        p = torch.as_tensor(state_particles, dtype=torch.float32).to(self.device).reshape(-1, N * D).contiguous()
+        if f.shape[0] != p.shape[0]:
+            raise ValueError(f"state_features has {f.shape[0]} rows, state_particles {p.shape[0]}")
+        loss = C.c_double() if stats else None
+        with self._torch_order():
+            check(self._lib.td3_actor_learn_particles(self._h, f.data_ptr(), p.data_ptr(), int(f.shape[0]),
+                                                      self._stream(), C.byref(loss) if stats else None),
+                  "td3_actor_learn_particles")
+        return float(loss.value) if stats else None
+
     def train_step(self, replay_buffer, batch_size=100, indices=None, noise=None, stats=False):
         """``train`` with optional injected sample indices / N(0,1) noise and loss read-back."""
         B, A = int(batch_size), self.action_dim

@@ -81,10 +81,14 @@ SIGNATURES = {
     "td3_eval_q": (C.c_int, [_P, _F, _F, _F, C.c_int]),
     "td3_train_step_batch_particles": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_int, _P, _F,
                                                  C.POINTER(td3_step_stats)]),
+    "td3_actor_learn_particles": (C.c_int, [_P, _P, _P, C.c_int, _P, _D]),
     "td3_select_action_particles": (C.c_int, [_P, _F, _F, _F, C.c_int]),
     "td3_eval_q_particles": (C.c_int, [_P, _F, _F, _F, _F, C.c_int]),
     "td3_comm_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
     "td3_comm_init": (C.c_int, [_P, C.POINTER(C.c_ubyte), C.c_int, C.c_int]),
+    "td3_comm_init_local": (C.c_int, [C.POINTER(_P), C.c_int]),
+    "td3_train_step_local": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int, _I64, _F,
+                                       C.POINTER(td3_step_stats)]),
     "td3_sync": (C.c_int, [_P]),
     "td3_stream": (_P, [_P]),
     "td3_profile_stages": (C.c_int, [_P, _P, C.c_int, C.c_int, _F, C.c_int, C.POINTER(C.c_int)]),

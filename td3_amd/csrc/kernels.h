@@ -198,6 +198,8 @@ struct DwProb {
                                   // vector tiles: Np/32
   const float* rs; int ldrs;      // row scale of dZ / dU (unit-gradient backward): rs[r * ldrs];
                                   // ldrs = 0 with rs -> 1.0f when the rows are the gradients
+  int kvalid;                     // weight columns >= kvalid get a zero gradient: their U columns
+                                  // may hold another field (the actor reads [s | a] rows, ld pad32(sd+ad))
 };
 
 enum DwMode : int { kDwGrad = 0, kDwAdam = 1, kDwAdamPolyak = 2 };
@@ -220,6 +222,9 @@ struct DwArgs {
 };
 
 // ------------------------------------------------------------------ launchers (kernels.hip)
+// launch_gemm's bump_actor: 0 bumps total_it / critic_step, 1 also actor_step, kBumpActorOnly only
+// actor_step (TD3_particles._actor_learn outside a train step: the actor's Adam step, no total_it)
+constexpr int kBumpActorOnly = 2;
 int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds_bytes,
                 Counters* bump, int bump_actor, hipStream_t s);
 // Two independent GEMM stages in one launch (stage 2's tile ids follow stage 1's); only the pairs
@@ -234,6 +239,15 @@ int launch_heads(const HeadArgs& a, int nprob, hipStream_t s);
 int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s);
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s);
 int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s);
+// Data-parallel replicas in one process (td3_comm_init_local): arena k <- sum over j of arena j,
+// summed in replica order (the same value lands in every replica, like a ring all-reduce).
+constexpr int kMaxLocalReplicas = 8;
+struct LocalSumArgs {
+  float* a[kMaxLocalReplicas];
+  int n;
+  int64_t size;
+};
+int launch_local_sum(const LocalSumArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ weight normalization
 // norm = "weight_normalization" (TD3_featured.py:33-35, 68-70: torch weight_norm, dim 0, on

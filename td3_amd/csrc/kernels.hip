@@ -1106,7 +1106,6 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_kernel2(int Bp, int n1, Ge
 //  4. WK > 1: the partial tiles are summed through LDS; bias / ReLU epilogue.
 // With kNW waves, a wave holds at most 16 / kNW chunks of K <= 512 (WN = 1: WK = kNW;
 // WN = 4 only runs K <= 128 with WK = kNW / 4).
-constexpr int kMaxChunks = 16 / kNW;
 
 template <int MODE>
 __device__ __forceinline__ void load_chunk(const GemmProb& P, float (&b)[16], int ch, int ncol, int h) {
@@ -1466,10 +1465,12 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
   // step counters (TD3_featured.py:124), off the head of the chain; the bumping stage never
   // reads them (the sample of this step drew its rows in the stage before)
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
-    bump->total_it += 1;
-    bump->critic_step += 1;
-    bump->pw[0] *= bump->beta[0];
-    bump->pw[1] *= bump->beta[1];
+    if (bump_actor != kBumpActorOnly) {
+      bump->total_it += 1;
+      bump->critic_step += 1;
+      bump->pw[0] *= bump->beta[0];
+      bump->pw[1] *= bump->beta[1];
+    }
     if (bump_actor) {
       bump->actor_step += 1;
       bump->pw[2] *= bump->beta[2];
@@ -2011,7 +2012,7 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
       float g = red[tn * 33 + tq + q];
 #pragma unroll
       for (int w = 1; w < 4; ++w) g = g + red[(w * 32 + tn) * 33 + tq + q];
-      gq[q] = g;
+      gq[q] = k0 + tq + q < P.kvalid ? g : 0.f;     // zero gradient, zero moments: the pad stays 0
     }
     if (grad_only) {
       gst4(a.adam.G + ix, make_float4(gq[0], gq[1], gq[2], gq[3]));
@@ -2169,7 +2170,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
     for (int r = 0; r < 16; ++r) {
       const int n = n0 + qn * 32 + mfma_row(r, lane);
       gq[r] = acc[r] + red[mfma_row(r, lane) * 33 + i];
-      ok[r] = n < P.Np && kk < P.Kp;
+      ok[r] = n < P.Np && kk < P.kvalid;           // kvalid <= Kp: columns past it keep their 0
       idx[r] = P.offW + (int64_t)n * P.Kp + kk;
     }
     TL_MARK(2);
@@ -2306,7 +2307,7 @@ __global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
     for (int r = 0; r < 16; ++r) {
       const int n = n0 + qn * 32 + mfma_row(r, lane);
       gq[r] = acc[r] + red[mfma_row(r, lane) * 33 + i];
-      ok[r] = n < P.Np && kk < P.Kp;
+      ok[r] = n < P.Np && kk < P.kvalid;           // kvalid <= Kp: columns past it keep their 0
       idx[r] = P.offW + (int64_t)n * P.Kp + kk;
     }
     TL_MARK(2);
@@ -2320,6 +2321,14 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, i
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float g = gld(a.G + (i)) * k.gscale;
     adam_elem(a.P + i, a.M + i, a.V + i, g, k, polyak ? a.T + i : nullptr);
+  }
+}
+
+__global__ __launch_bounds__(256) void local_sum_kernel(LocalSumArgs a) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.size; i += (int64_t)gridDim.x * 256) {
+    float v = gld(a.a[0] + i);
+    for (int k = 1; k < a.n; ++k) v = v + gld(a.a[k] + i);
+    for (int k = 0; k < a.n; ++k) gst(a.a[k] + i, v);
   }
 }
 
@@ -2691,6 +2700,17 @@ int launch_wn(const WnArgs& a, hipStream_t s) {
       return -1;
     }
   hipLaunchKernelGGL(wn_kernel, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_local_sum(const LocalSumArgs& a, hipStream_t s) {
+  if (a.n < 1 || a.n > kMaxLocalReplicas || a.size < 0) {
+    set_error("launch_local_sum: %d replicas (max %d)", a.n, kMaxLocalReplicas);
+    return -1;
+  }
+  const int blocks = (int)std::min<int64_t>((a.size + 255) / 256, 2048);
+  if (blocks > 0) hipLaunchKernelGGL(local_sum_kernel, dim3(blocks), dim3(256), 0, s, a);
   TD3_HIP(hipGetLastError());
   return 0;
 }

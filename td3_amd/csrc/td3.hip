@@ -185,6 +185,14 @@ struct Stage {
   double flops = 0;
   std::string kernel;   // HIP kernel function the stage launches (rocprof name)
   std::shared_ptr<GemmLaunch> gemm;   // GEMM stages only
+  int collective = -1;  // data parallel: the gradient all-reduce of group 0 (actor) / 1 (critic)
+};
+
+// Replicas of one process sharing a device (td3_comm_init_local): the test seam of the data-parallel
+// path.  Their steps run stage by stage on one stream (td3_train_step_local), and each all-reduce
+// is a fixed-order device sum over the replicas' G arenas in place of ncclAllReduce.
+struct LocalGroup {
+  std::vector<td3_handle*> hs;
 };
 
 struct Plan {
@@ -192,8 +200,8 @@ struct Plan {
   float* scratch = nullptr;
   size_t scratch_bytes = 0;
   // inputs
-  float *X_S = nullptr, *X_SA = nullptr, *X_S2 = nullptr, *X_S2A = nullptr, *X_SP = nullptr;
-  int ld_s = 0, ld_sa = 0;
+  float *X_SA = nullptr, *X_S2A = nullptr, *X_SP = nullptr;
+  int ld_sa = 0;
   float *R = nullptr, *ND = nullptr, *noise = nullptr, *Y = nullptr, *sqerr = nullptr;
   float* gscale[2] = {};                // [Bp] g_r = 2/B (Q_j,r - y_r): row scale of Q_j's unit backward
   int64_t* d_idx = nullptr;
@@ -227,6 +235,8 @@ struct Plan {
   uint64_t src_key = 0;                 // Ring::gen of the source ring, kBatchSource for pbatch
   int nwg = 0;                          // encoder-backward workgroups per role per critic network
   int nwg_a = 0;                        // ... for the actor's encoder (one network per launch)
+  // TD3_particles._actor_learn(state_features, state_particles) on its own (TD3_particles.py:209-224)
+  std::vector<Stage> actor_learn;
 };
 
 // Query batches up to this many (padded) rows keep their inputs and outputs in mapped pinned host
@@ -316,8 +326,10 @@ struct td3_handle {
   std::unique_ptr<Plan> plan;
   std::map<int, std::unique_ptr<ActPlan>> act;
   ncclComm_t comm = nullptr;
+  std::shared_ptr<LocalGroup> local;          // td3_comm_init_local (comm stays null)
   int nranks = 1, rank = 0;
   std::vector<Stage>* last_body = nullptr;
+  Ring* last_ring = nullptr;                  // the ring of the last td3_profile_stages (stage 0: its gather)
   std::vector<std::string> stage_names;
   std::vector<std::string> stage_kernels;
 };
@@ -790,6 +802,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
         p.offg = -1;
         p.offbeta = -1;
       }
+      p.kvalid = L.K;                  // layer 0 may read a wider row (the actor's [s | a] input)
       p.ntk = tile64 ? (L.Kp + 63) / 64 : L.Kp / 32;
       p.tile_begin = blocks;
       blocks += (tile64 ? (L.Np + 63) / 64 : L.Np / 32) * p.ntk + L.Np / 32;   // matrix, then vector tiles
@@ -810,6 +823,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       p.ldh = it.e->ldx;
       p.stats = it.e->statsIn;
       p.ntk = 0;
+      p.kvalid = 0;
       p.tile_begin = blocks;
       blocks += p.Np / 32;
       probs.push_back(p);
@@ -833,7 +847,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.adam.eps = h->adam[which].eps;
   a.adam.tau = (float)h->cfg.tau;
   a.adam.grad_scale = 1.0f;
-  const bool dp = h->comm != nullptr;
+  const bool dp = h->comm != nullptr || h->local != nullptr;
   const bool wn = g.wn.nlin > 0;            // weight normalization: dW -> (dg, dv) in wn_kernel
   a.mode = (dp || wn) ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
   a.tile64 = tile64 ? 1 : 0;
@@ -860,8 +874,13 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     ncclComm_t comm = h->comm;
     float* G = g.G;
     const int64_t n = g.size;
+    const bool local = h->local != nullptr;
     st.push_back({std::string(tag) + "_allreduce",
                   [=](hipStream_t s) {
+                    if (local) {
+                      set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
+                      return -1;
+                    }
                     ncclResult_t r = ncclAllReduce(G, G, (size_t)n, ncclFloat, ncclSum, comm, s);
                     if (r != ncclSuccess) {
                       set_error("ncclAllReduce: %s", ncclGetErrorString(r));
@@ -870,6 +889,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                     return 0;
                   },
                   0, "rccl"});
+    st.back().collective = which == 1 ? 0 : 1;     // AdamArgs::which 1 = actor -> group 0
   }
   AdamArgs aa = a.adam;
   if (dp) aa.grad_scale = 1.0f / (float)h->nranks;
@@ -934,13 +954,12 @@ static int build_step(td3_handle* h, int B) {
   P->Bp = Bp;
   const bool norm = h->cfg.norm == 1;
   const int sd = h->sd, ad = h->ad;
-  P->ld_s = pad32(sd);
   P->ld_sa = pad32(sd + ad);
   P->fuse_gather = 2 * sd + ad + 2 <= 128;
   const NetL& an = h->actor.nets[0];
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[1];
-  size_t floats = (size_t)Bp * (2 * P->ld_s + 3 * P->ld_sa) + 10 * (size_t)Bp + (size_t)Bp * ad + 4096;
+  size_t floats = (size_t)Bp * 3 * P->ld_sa + 10 * (size_t)Bp + (size_t)Bp * ad + 4096;
   floats += eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, true, norm) +
             eval_floats(an, Bp, true, norm) + 2 * eval_floats(q1, Bp, false, norm) +
             eval_floats(q1, Bp, true, norm) + 1024;
@@ -949,8 +968,9 @@ static int build_step(td3_handle* h, int B) {
   TD3_HIP(hipMemset(P->scratch, 0, P->scratch_bytes));
   TD3_HIP(hipDeviceSynchronize());   // null-stream memset vs the non-blocking step stream
   Scratch S{P->scratch, floats, 0};
-  P->X_S = S.take((size_t)Bp * P->ld_s);
-  P->X_S2 = S.take((size_t)Bp * P->ld_s);
+  // network inputs: [s | a] (twin, and the actor reads its first sd columns: the dW of its layer 0
+  // masks columns >= sd, DwProb::kvalid), [s' | a'] (target twin; the target actor reads s' there),
+  // [s | pi(s)] (Q1 of the actor loss).  Columns past a row's fields are zero.
   P->X_SA = S.take((size_t)Bp * P->ld_sa);
   P->X_S2A = S.take((size_t)Bp * P->ld_sa);
   P->X_SP = S.take((size_t)Bp * P->ld_sa);
@@ -963,10 +983,10 @@ static int build_step(td3_handle* h, int B) {
   P->d_inject_idx = (int64_t*)S.take(2 * (size_t)Bp);
   P->gscale[0] = S.take(Bp);
   P->gscale[1] = S.take(Bp);
-  alloc_eval(S, an, Bp, P->X_S2, P->ld_s, false, norm, false, P->TA);
+  alloc_eval(S, an, Bp, P->X_S2A, P->ld_sa, false, norm, false, P->TA);
   alloc_eval(S, q1, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[0]);
   alloc_eval(S, q2, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[1]);
-  alloc_eval(S, an, Bp, P->X_S, P->ld_s, true, norm, true, P->A);
+  alloc_eval(S, an, Bp, P->X_SA, P->ld_sa, true, norm, true, P->A);
   alloc_eval(S, q1, Bp, P->X_S2A, P->ld_sa, false, norm, true, P->TQ[0]);
   alloc_eval(S, q2, Bp, P->X_S2A, P->ld_sa, false, norm, true, P->TQ[1]);
   alloc_eval(S, q1, Bp, P->X_SP, P->ld_sa, true, norm, true, P->AQ);
@@ -1028,8 +1048,8 @@ static int build_step(td3_handle* h, int B) {
       TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase, nullptr, nullptr, 0, true));
       {  // the ring-sampled first layer (record layout [s | a | s' | r | not_done], replay.hip)
         // the first column tile of each problem keeps what the later stages read: the target-twin
-        // input s' (X_S2A), the twin dW input [s | a] (X_SA), reward / not_done, and on policy
-        // steps the actor dW input s (X_S) and the policy-Q input s (X_SP)
+        // input s' (X_S2A), the twin (and actor) dW input [s | a] (X_SA), reward / not_done, and on
+        // policy steps the policy-Q input s (X_SP)
         std::vector<FwdItem> f1r = f1;
         f1r[0].ring_src = sd + ad;                   // target actor on s'
         f1r[1].ring_src = 0;                         // twin on [s | a]
@@ -1039,7 +1059,7 @@ static int build_step(td3_handle* h, int B) {
         RingOut ro[4] = {{P->X_S2A, P->ld_sa, nullptr, 0, nullptr, nullptr},
                          {P->X_SA, P->ld_sa, nullptr, 0, nullptr, nullptr},
                          {nullptr, 0, nullptr, 0, P->R, P->ND},
-                         {P->X_S, P->ld_s, P->X_SP, P->ld_sa, nullptr, nullptr}};
+                         {P->X_SP, P->ld_sa, nullptr, 0, nullptr, nullptr}};
         TD3_RC(add_fwd_stages(h, P->tables, fr, f1r, Bp, B, "F", h->d_ctr, actor_phase, &P->rside, ro,
                               2 * sd + ad, true));
         P->body_ring[actor_phase][inj].push_back(fr[0]);
@@ -1451,6 +1471,70 @@ static int build_step_particles(td3_handle* h, int B) {
     return p;
   };
 
+  // ---------------- delayed policy update (TD3_particles.py:206-224): _actor_learn on (s features, s
+  // particles) with the post-step critic; A_dw also runs the actor's Polyak (the critic's is in C_dw)
+  auto actor_phase_stages = [&](std::vector<Stage>& st) -> int {
+    Plan* Pp = P.get();
+    push_enc_fwd(h, Pp, st, {{&q1, Pq, P->XAQ, P->ld_q, 0, nullptr}}, "AF_enc");
+    std::vector<FwdItem> f3 = {{&q1, Pq, &P->AQ, false, true}};
+    TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0));
+    {
+      GemmProb p{};
+      p.norm = norm ? 1 : 0;
+      p.B = B;
+      p.ex[0] = P->AQ.H[2];
+      p.ex[1] = const_cast<float*>(Pq + q1.ln[2].offg);
+      p.ex[2] = const_cast<float*>(Pq + q1.ln[2].offb);
+      p.ex[3] = const_cast<float*>(Pq + q1.lin[3].offW);
+      p.ex[4] = const_cast<float*>(Pq + q1.lin[3].offb);
+      p.ex[5] = P->AQ.Qv;
+      p.Aout = P->AQ.GZ[2];
+      p.ldao = q1.lin[2].Np;
+      p.exi[0] = q1.lin[2].N;
+      p.exi[1] = q1.lin[2].Np;
+      p.exi[2] = ad;
+      p.exi[3] = q1.lin[3].Kp;
+      p.exf[0] = (float)(-1.0 / ((double)B * ad));
+      std::vector<GemmProb> v = {p};
+      TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorLossP, Bp, "actor_loss"));
+    }
+    std::vector<BwdItem> aqb = {{&q1, Pq, &P->AQ, false}};
+    TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false, true));
+    {
+      GemmProb p{};
+      p.norm = norm ? 1 : 0;
+      p.B = B;
+      p.ex[0] = P->AQ.GUin;
+      p.ex[1] = P->XAQ;
+      p.ex[2] = P->AQ.statsIn;
+      p.ex[3] = const_cast<float*>(Pq + q1.ln_in.offg);
+      p.ex[5] = P->A.T;
+      p.ex[6] = const_cast<float*>(Pa + an.lin[3].offW);
+      p.ex[7] = P->A.H[2];
+      p.ex[8] = P->A.stats[2];
+      p.ex[9] = const_cast<float*>(Pa + an.ln[2].offg);
+      p.ex[10] = P->A.GZ[3];
+      p.ex[11] = P->A.GU[2];
+      p.Aout = P->A.GZ[2];
+      p.ldao = an.lin[2].Np;
+      p.exi[0] = q1.lin[0].K;
+      p.exi[1] = q1.lin[0].Kp;
+      p.exi[3] = acol;
+      p.exi[4] = ad;
+      p.exi[5] = an.lin[2].N;
+      p.exi[6] = an.lin[2].Np;
+      p.exi[7] = an.lin[3].Kp;
+      p.exf[0] = 1.0f;
+      std::vector<GemmProb> v = {p};
+      TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorHeadBwdP, Bp, "actor_head_bwd"));
+    }
+    std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
+    TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true, true));
+    push_enc_bwd(h, Pp, st, ab, {P->XA}, "AB_enc");
+    TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, P->nwg_a));
+    return 0;
+  };
+
   for (int actor_phase = 0; actor_phase < 2; ++actor_phase) {
     for (int inj = 0; inj < 2; ++inj) {
       std::vector<Stage>& st = P->body[actor_phase][inj];
@@ -1536,65 +1620,25 @@ static int build_step_particles(td3_handle* h, int B) {
       push_enc_bwd(h, Pp, st, cb, cbx, "CB_enc");
       TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, P->nwg));
       if (!actor_phase) continue;
-      // ---------------- delayed policy update (TD3_particles.py:206-224)
-      push_enc_fwd(h, Pp, st, {{&q1, Pq, P->XAQ, P->ld_q, 0, nullptr}}, "AF_enc");
-      std::vector<FwdItem> f3 = {{&q1, Pq, &P->AQ, false, true}};
-      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0));
-      {
-        GemmProb p{};
-        p.norm = norm ? 1 : 0;
-        p.B = B;
-        p.ex[0] = P->AQ.H[2];
-        p.ex[1] = const_cast<float*>(Pq + q1.ln[2].offg);
-        p.ex[2] = const_cast<float*>(Pq + q1.ln[2].offb);
-        p.ex[3] = const_cast<float*>(Pq + q1.lin[3].offW);
-        p.ex[4] = const_cast<float*>(Pq + q1.lin[3].offb);
-        p.ex[5] = P->AQ.Qv;
-        p.Aout = P->AQ.GZ[2];
-        p.ldao = q1.lin[2].Np;
-        p.exi[0] = q1.lin[2].N;
-        p.exi[1] = q1.lin[2].Np;
-        p.exi[2] = ad;
-        p.exi[3] = q1.lin[3].Kp;
-        p.exf[0] = (float)(-1.0 / ((double)B * ad));
-        std::vector<GemmProb> v = {p};
-        TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorLossP, Bp, "actor_loss"));
-      }
-      std::vector<BwdItem> aqb = {{&q1, Pq, &P->AQ, false}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, aqb, Bp, B, "AQB", false, true));
-      {
-        GemmProb p{};
-        p.norm = norm ? 1 : 0;
-        p.B = B;
-        p.ex[0] = P->AQ.GUin;
-        p.ex[1] = P->XAQ;
-        p.ex[2] = P->AQ.statsIn;
-        p.ex[3] = const_cast<float*>(Pq + q1.ln_in.offg);
-        p.ex[5] = P->A.T;
-        p.ex[6] = const_cast<float*>(Pa + an.lin[3].offW);
-        p.ex[7] = P->A.H[2];
-        p.ex[8] = P->A.stats[2];
-        p.ex[9] = const_cast<float*>(Pa + an.ln[2].offg);
-        p.ex[10] = P->A.GZ[3];
-        p.ex[11] = P->A.GU[2];
-        p.Aout = P->A.GZ[2];
-        p.ldao = an.lin[2].Np;
-        p.exi[0] = q1.lin[0].K;
-        p.exi[1] = q1.lin[0].Kp;
-        p.exi[3] = acol;
-        p.exi[4] = ad;
-        p.exi[5] = an.lin[2].N;
-        p.exi[6] = an.lin[2].Np;
-        p.exi[7] = an.lin[3].Kp;
-        p.exf[0] = 1.0f;
-        std::vector<GemmProb> v = {p};
-        TD3_RC(push_row_stage(h, P->tables, st, v, kRowActorHeadBwdP, Bp, "actor_head_bwd"));
-      }
-      std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
-      TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true, true));
-      push_enc_bwd(h, Pp, st, ab, {P->XA}, "AB_enc");
-      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, P->nwg_a));
+      TD3_RC(actor_phase_stages(st));
     }
+  }
+  {   // _actor_learn called on its own (evaluate_model.py:39-49): the actor's forward on s, pi(s),
+      // then the policy-step stages; the step counter of the actor's Adam only (no total_it), and
+      // the critic's Polyak as a flat pass (TD3_particles.py:219-221; inside a train step C_dw does it)
+    std::vector<Stage>& st = P->actor_learn;
+    push_enc_fwd(h, P.get(), st, {{&an, Pa, P->XA, P->ld_a, 0, P->A.mask}}, "L_enc");
+    std::vector<FwdItem> f1 = {{&an, Pa, &P->A, true, true}};
+    TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "L", h->d_ctr, kBumpActorOnly));
+    std::vector<GemmProb> hp = {policy_head(Pa, P->A, P->XAQ, nullptr, 0, 0)};
+    TD3_RC(push_row_stage(h, P->tables, st, hp, kRowPolicyHead, Bp, "L_head"));
+    TD3_RC(actor_phase_stages(st));
+    float* Tc = h->critic.T;
+    const float* Pc = h->critic.P;
+    const int64_t nc = h->critic.size;
+    const float tau = (float)h->cfg.tau;
+    st.push_back({"L_polyak_critic", [=](hipStream_t s) { return launch_polyak_flat(Tc, Pc, nc, tau, s); }, 0,
+                  "td3::polyak_flat_kernel"});
   }
   if (h->plan) destroy_plan(h->plan.get());
   h->plan = std::move(P);
@@ -1614,11 +1658,11 @@ static int input_from_ring(td3_handle* h, Ring* r, Plan* P, bool inject_idx, hip
   GatherArgs a{};
   const int sd = h->sd, ad = h->ad;
   int k = 0;
-  a.seg[k++] = GatherSeg{P->X_S, P->ld_s, 0, r->o_s, sd};
+  // s once per network input that holds it ([s | a] and [s | pi(s)]), s' once ([s' | a']): the
+  // actors read the state columns of those rows (build_step)
   a.seg[k++] = GatherSeg{P->X_SA, P->ld_sa, 0, r->o_s, sd};
   a.seg[k++] = GatherSeg{P->X_SA, P->ld_sa, sd, r->o_a, ad};
   a.seg[k++] = GatherSeg{P->X_SP, P->ld_sa, 0, r->o_s, sd};
-  a.seg[k++] = GatherSeg{P->X_S2, P->ld_s, 0, r->o_s2, sd};
   a.seg[k++] = GatherSeg{P->X_S2A, P->ld_sa, 0, r->o_s2, sd};
   a.seg[k++] = GatherSeg{P->R, 1, 0, r->o_r, 1};
   a.seg[k++] = GatherSeg{P->ND, 1, 0, r->o_nd, 1};
@@ -1680,12 +1724,12 @@ __global__ void pack_kernel(const float* __restrict__ src, int cols, int B, int 
 static int input_from_batch(td3_handle* h, Plan* P, const float* s, const float* a, const float* s2,
                             const float* r, const float* nd, hipStream_t st) {
   const int sd = h->sd, ad = h->ad, Bp = P->Bp, B = P->B;
-  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, s, sd, B, Bp, P->X_S, P->ld_s, 0,
-                     P->X_SA, P->ld_sa, 0, P->X_SP, P->ld_sa, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, s, sd, B, Bp, P->X_SA, P->ld_sa, 0,
+                     P->X_SP, P->ld_sa, 0, (float*)nullptr, 0, 0);
   hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, a, ad, B, Bp, P->X_SA, P->ld_sa, sd,
                      (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
-  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, s2, sd, B, Bp, P->X_S2, P->ld_s, 0,
-                     P->X_S2A, P->ld_sa, 0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, s2, sd, B, Bp, P->X_S2A, P->ld_sa, 0,
+                     (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
   hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, r, 1, B, Bp, P->R, 1, 0,
                      (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
   hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, st, nd, 1, B, Bp, P->ND, 1, 0,
@@ -1697,6 +1741,10 @@ static int input_from_batch(td3_handle* h, Plan* P, const float* s, const float*
 // One step body on stream s.  With `ring` set, the replay-ring gather (Philox draw) is
 // launched first and, in graph mode, captured into the same hipGraph (one replay per step).
 static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring* ring) {
+  if (h->local) {
+    set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
+    return -1;
+  }
   Plan* P = h->plan.get();
   const bool fused = ring && P->fuse_gather;     // featured: the sample runs inside F_fwd0
   std::vector<Stage>& st = fused ? P->body_ring[actor_phase][inj] : P->body[actor_phase][inj];
@@ -2249,6 +2297,9 @@ int td3_destroy(td3_handle* h) {
     if (kv.second->hio) (void)hipHostFree(kv.second->hio);
   }
   if (h->comm) ncclCommDestroy(h->comm);
+  if (h->local)       // the group loses a member: the rest refuse td3_train_step_local from now on
+    for (auto& m : h->local->hs)
+      if (m == h) m = nullptr;
   (void)hipFree(h->arena);
   (void)hipFree(h->d_ctr);
   (void)hipFree(h->ones);
@@ -2610,6 +2661,40 @@ int td3_train_step_batch_particles(td3_handle* h, const float* feat, const float
   return finish_step(h, actor_phase, s, stats);
 }
 
+int td3_actor_learn_particles(td3_handle* h, const float* feat, const float* part, int batch, void* stream,
+                              double* actor_loss) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_ARG(h->particles, "td3_actor_learn_particles on a featured learner (TD3_featured has no _actor_learn)");
+  TD3_ARG(feat && part, "null input");
+  TD3_ARG(batch > 0, "batch must be positive");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_RC(ensure_plan(h, batch));
+  Plan* P = h->plan.get();
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  const int F = h->sd, B = P->B, Bp = P->Bp, np = h->N * h->D, c0 = kEncC2;
+  set_particle_source(P, kBatchSource, P->pbatch, 2 * np, 0, np, P->d_iota);
+  // (features -> the actor's and Q1(s, pi)'s MLP input rows, particles -> the packed rows the
+  // encoders read; the actions of Q1(s, pi) are written by the policy head)
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, feat, F, B, Bp, P->XA, P->ld_a, c0, P->XAQ, P->ld_q,
+                     c0, (float*)nullptr, 0, 0);
+  hipLaunchKernelGGL(pack_kernel, dim3(Bp), dim3(64), 0, s, part, np, B, Bp, P->pbatch, 2 * np, 0,
+                     (float*)nullptr, 0, 0, (float*)nullptr, 0, 0);
+  TD3_HIP(hipGetLastError());
+  TD3_RC(run_stages(P->actor_learn, s));
+  h->last_step_stream = s;
+  h->actor_step += 1;
+  if (h->act_used) TD3_HIP(hipEventRecord(h->actor_ev, s));
+  if (!actor_loss) return 0;
+  TD3_HIP(hipStreamSynchronize(s));
+  const int nq = P->nq, ldq = P->ldq;
+  std::vector<float> q((size_t)B * nq);
+  TD3_HIP(hipMemcpy2D(q.data(), (size_t)nq * 4, P->AQ.Qv, (size_t)ldq * 4, (size_t)nq * 4, B, hipMemcpyDeviceToHost));
+  double m = 0;
+  for (float v : q) m += v;
+  *actor_loss = -m / ((double)B * nq);
+  return 0;
+}
+
 int td3_select_action_particles(td3_handle* h, const float* feat, const float* part, float* action_out, int n) {
   TD3_ARG(h && feat && part && action_out, "null argument");
   TD3_ARG(h->particles, "not a particle learner");
@@ -2694,6 +2779,106 @@ int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int ra
   return 0;
 }
 
+int td3_comm_init_local(td3_handle** hs, int n) {
+  TD3_ARG(hs != nullptr, "null argument");
+  TD3_ARG(n >= 1 && n <= kMaxLocalReplicas, "1 .. 8 local replicas");
+  for (int k = 0; k < n; ++k) {
+    TD3_ARG(hs[k] != nullptr, "null handle");
+    TD3_ARG(!hs[k]->comm && !hs[k]->local, "handle already in a data-parallel group");
+    TD3_ARG(hs[k]->cfg.device == hs[0]->cfg.device, "local replicas share one device");
+    TD3_ARG(hs[k]->particles == hs[0]->particles && hs[k]->actor.size == hs[0]->actor.size &&
+                hs[k]->critic.size == hs[0]->critic.size && hs[k]->cfg.norm == hs[0]->cfg.norm,
+            "local replicas must have the same configuration");
+    for (int j = 0; j < k; ++j) TD3_ARG(hs[j] != hs[k], "a handle appears twice");
+  }
+  auto g = std::make_shared<LocalGroup>();
+  g->hs.assign(hs, hs + n);
+  for (int k = 0; k < n; ++k) {
+    td3_handle* h = hs[k];
+    TD3_HIP(hipSetDevice(h->cfg.device));
+    TD3_HIP(hipStreamSynchronize(h->stream));
+    h->local = g;
+    h->nranks = n;
+    h->rank = k;
+    if (h->plan) TD3_RC(build_plan(h, h->plan->B));   // grad-only dW + all-reduce + flat Adam
+  }
+  return 0;
+}
+
+int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, const int64_t* inject_idx,
+                         const float* inject_noise, td3_step_stats* stats) {
+  TD3_ARG(hs && rbs && n >= 1 && hs[0], "null argument");
+  TD3_ARG(batch > 0, "batch must be positive");
+  std::shared_ptr<LocalGroup> g = hs[0]->local;
+  TD3_ARG(g && (int)g->hs.size() == n, "handles are not one td3_comm_init_local group");
+  for (int k = 0; k < n; ++k) {
+    TD3_ARG(hs[k] == g->hs[k], "handles must be passed in the group's rank order");
+    TD3_ARG(rbs[k] != nullptr, "null replay buffer");
+    TD3_ARG(hs[k]->total_it == hs[0]->total_it, "replicas out of step");
+  }
+  td3_handle* h0 = hs[0];
+  TD3_HIP(hipSetDevice(h0->cfg.device));
+  hipStream_t s = h0->stream;            // every replica's stages in one stream order
+  for (int k = 0; k < n; ++k) {
+    td3_handle* h = hs[k];
+    Ring* r = reinterpret_cast<Ring*>(rbs[k]);
+    TD3_ARG(r->sd == h->sd && r->ad == h->ad && r->particles == h->particles, "replay buffer does not match");
+    TD3_ARG(r->size > 0 || inject_idx, "train on an empty replay buffer");
+    TD3_ARG(r->device == h->cfg.device, "replay buffer lives on another device");
+    if (h->stream != s) TD3_HIP(hipStreamSynchronize(h->stream));
+    TD3_RC(ensure_plan(h, batch));
+    TD3_RC(bind_ring(h, r));
+    TD3_RC(ring_begin_read(r, s));
+  }
+  const int actor_phase = ((h0->total_it + 1) % h0->cfg.policy_freq) == 0;
+  const int inj = inject_noise ? 1 : 0;
+  std::vector<std::vector<Stage>*> lists(n);
+  std::vector<size_t> pos(n, 0);
+  for (int k = 0; k < n; ++k) {
+    td3_handle* h = hs[k];
+    Plan* P = h->plan.get();
+    Ring* r = reinterpret_cast<Ring*>(rbs[k]);
+    if (inject_idx) {
+      for (int i = 0; i < batch; ++i)
+        TD3_ARG(inject_idx[(size_t)k * batch + i] >= 0 && inject_idx[(size_t)k * batch + i] < r->cap,
+                "injected index out of range");
+      TD3_HIP(hipMemcpyAsync(P->d_inject_idx, inject_idx + (size_t)k * batch, (size_t)batch * 8,
+                             hipMemcpyHostToDevice, s));
+    }
+    if (inject_noise)
+      TD3_HIP(hipMemcpyAsync(P->noise, inject_noise + (size_t)k * batch * h->ad, (size_t)batch * h->ad * 4,
+                             hipMemcpyHostToDevice, s));
+    const bool fused = !inject_idx && P->fuse_gather;
+    if (!fused) TD3_RC(input_from_ring(h, r, P, inject_idx != nullptr, s));
+    lists[k] = fused ? &P->body_ring[actor_phase][inj] : &P->body[actor_phase][inj];
+    h->last_body = lists[k];
+  }
+  for (;;) {
+    int coll = -2;
+    for (int k = 0; k < n; ++k) {
+      std::vector<Stage>& st = *lists[k];
+      while (pos[k] < st.size() && st[pos[k]].collective < 0) TD3_RC(st[pos[k]++].run(s));
+      const int c = pos[k] < st.size() ? st[pos[k]].collective : -1;
+      TD3_ARG(k == 0 || c == coll, "internal: replicas reached different collectives");
+      coll = c;
+    }
+    if (coll < 0) break;
+    LocalSumArgs a{};
+    a.n = n;
+    for (int k = 0; k < n; ++k) {
+      Group& grp = coll == 0 ? hs[k]->actor : hs[k]->critic;
+      a.a[k] = grp.G;
+      a.size = grp.size;
+      ++pos[k];
+    }
+    TD3_RC(launch_local_sum(a, s));
+  }
+  for (int k = 0; k < n; ++k) TD3_RC(ring_end_read(reinterpret_cast<Ring*>(rbs[k]), s));
+  if (inject_idx || inject_noise) TD3_HIP(hipStreamSynchronize(s));
+  for (int k = 0; k < n; ++k) TD3_RC(finish_step(hs[k], actor_phase, s, stats ? &stats[k] : nullptr));
+  return 0;
+}
+
 int td3_sync(td3_handle* h) {
   TD3_ARG(h != nullptr, "null handle");
   TD3_HIP(hipSetDevice(h->cfg.device));
@@ -2742,6 +2927,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   for (auto& e : ev) (void)hipEventDestroy(e);
   *n_stages = n;
   h->last_body = &st;
+  h->last_ring = r;
   // the profiled step is a real step: keep the host mirror in sync
   h->total_it += 1;
   h->critic_step += 1;
@@ -2767,10 +2953,18 @@ double td3_stage_flops(td3_handle* h, int i) {
 int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean) {
   TD3_ARG(h && ms_mean, "null argument");
   TD3_ARG(h->last_body != nullptr, "run td3_profile_stages first");
-  TD3_ARG(stage >= 1 && stage <= (int)h->last_body->size(), "stage index out of range");
+  TD3_ARG(stage >= 0 && stage <= (int)h->last_body->size(), "stage index out of range");
   TD3_ARG(iters > 0, "iters must be positive");
+  TD3_ARG(stage > 0 || h->last_ring, "stage 0 (the gather) needs the ring of td3_profile_stages");
   TD3_HIP(hipSetDevice(h->cfg.device));
-  Stage& st = (*h->last_body)[stage - 1];
+  // stage 0: the stand-alone gather (Philox draw + record reads + batch writes, gather_kernel) of
+  // the profiled ring -- a separate launch when the step samples it (Plan::fuse_gather false), the
+  // sample phase measured on its own otherwise
+  Ring* ring = h->last_ring;
+  Plan* plan = h->plan.get();
+  Stage gather{"gather", [=](hipStream_t s) { return input_from_ring(h, ring, plan, false, s); }, 0,
+               "td3::gather_kernel"};
+  Stage& st = stage ? (*h->last_body)[stage - 1] : gather;
   hipEvent_t a, b;
   TD3_HIP(hipEventCreate(&a));
   TD3_HIP(hipEventCreate(&b));

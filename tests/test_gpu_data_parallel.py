@@ -1,0 +1,132 @@
+"""The product's data-parallel path with more than one replica, on one MI355X.
+
+RCCL cannot put two ranks on one GPU, so n replicas of one process form a
+``td3_comm_init_local`` group: the same data-parallel stage lists as ``td3_comm_init`` (grad-only
+dW, all-reduce, flat Adam with grad scale 1/n, Polyak), with the all-reduce a fixed-order device sum
+over the replicas' gradient arenas.  Replica k samples its own ring at rows
+``idx[k*B/n:(k+1)*B/n]`` of a golden batch (TD3_featured.py:148-164; noise likewise).
+
+Checks, per step (teacher-forced from the oracle's state):
+* the replicas end bit-identical (actor, critic, targets, Adam moments);
+* they equal the oracle's ONE step on the concatenated global batch (SURVEY §8e equivalence:
+  the losses are batch means, so the mean of the shard gradients is the global gradient), at the
+  SURVEY §8c tolerances.
+"""
+import numpy as np
+import pytest
+
+from helpers import gen, orc, load_golden, featured_setup, particle_setup
+from test_gpu_parity import _make, _load_oracle_state, _params_close, _rel_to_max
+
+pytestmark = pytest.mark.gpu
+
+
+def _replicas(S, n, maker):
+    from td3_amd.data_parallel import local_group
+    pols, rbs = [], []
+    for _ in range(n):
+        p, rb = maker(S)
+        pols.append(p)
+        rbs.append(rb)
+    local_group(pols)
+    return pols, rbs
+
+
+def _all_views(pol):
+    from td3_amd import _lib
+    from td3_amd.TD3_featured import _ParamView
+    return [pol.actor.flat(), pol.critic.flat(), pol.actor_target.flat(), pol.critic_target.flat(),
+            _ParamView(pol, _lib.TD3_ACTOR_ADAM_M, 0).flat(), _ParamView(pol, _lib.TD3_CRITIC_ADAM_V, 1).flat()]
+
+
+def _check_replicas_equal(pols):
+    ref = _all_views(pols[0])
+    for p in pols[1:]:
+        for a, b in zip(ref, _all_views(p)):
+            np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("name,n", [("hc_layer", 2), ("hc_layer", 4), ("hc_none", 2), ("hc_wn", 2)])
+def test_local_replicas_equal_global_batch_step(name, n):
+    from td3_amd.data_parallel import train_local
+    G = load_golden("featured", name)
+    S = featured_setup(name)
+    pols, rbs = _replicas(S, n, _make)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    B = S["B"]
+    b = B // n
+    for step in range(1, S["steps"] + 1):
+        p = f"step{step}"
+        idx, noise = G[f"{p}/idx"], G[f"{p}/noise"]
+        for pol in pols:
+            _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        outs = train_local(pols, rbs, b, indices=idx.reshape(n, b), noise=noise.reshape(n, b, -1), stats=True)
+        y = np.concatenate([o["y"][:, 0] for o in outs])
+        q1 = np.concatenate([o["q1"][:, 0] for o in outs])
+        assert _rel_to_max(y, rec["y"][:, 0]) <= 1e-5, (p, "y")
+        assert _rel_to_max(q1, rec["q1"][:, 0]) <= 1e-5, (p, "q1")
+        # each replica's loss is its shard's; their mean is the global batch-mean loss
+        np.testing.assert_allclose(np.mean([o["critic_loss"] for o in outs]), rec["critic_loss"], rtol=1e-5)
+        assert all(o["actor_step"] == ("actor_loss" in rec) for o in outs)
+        if "actor_loss" in rec:
+            np.testing.assert_allclose(np.mean([o["actor_loss"] for o in outs]), rec["actor_loss"],
+                                       rtol=1e-5, atol=1e-7)
+        _check_replicas_equal(pols)
+        pol = pols[0]
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (p, "critic"))
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"))
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (p, "actor"))
+        _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"))
+        assert all(q._counters() == (L.total_it, L.critic_step, L.actor_step) for q in pols)
+
+
+def test_local_replicas_free_running_philox():
+    """Production draws (each replica's Philox stream over its own ring, device noise): four
+    free-running steps keep the replicas bit-identical although their batches differ."""
+    from td3_amd.data_parallel import train_local
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+    from test_gpu_parity import Box
+    S = featured_setup("hc_layer")
+    pols, _ = _replicas(S, 2, _make)
+    rbs = []
+    data = gen.fill_featured_buffer(S["sd"], S["ad"], S["ma"], gen.BUFFER_ROWS, gen.SEED)
+    for seed in (11, 12):                  # one Philox stream per replica's ring
+        rb = ReplayBuffer_featured(Box((S["sd"],)), Box((S["ad"],)), max_size=gen.BUFFER_ROWS, seed=seed)
+        rb.add_batch(*data)
+        rbs.append(rb)
+    for _ in range(4):
+        outs = train_local(pols, rbs, 128, stats=True)
+        assert all(np.isfinite(o["critic_loss"]) for o in outs)
+    _check_replicas_equal(pols)
+
+
+def test_particle_local_replicas_equal_global_batch_step():
+    from test_gpu_particles import _make as make_particles
+    from td3_amd.data_parallel import train_local
+    G = load_golden("particles", "part_layer")
+    S = particle_setup("part_layer")
+    n, B = 2, S["B"]
+    b = B // n
+    pols, rbs = _replicas(S, n, make_particles)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    for step in range(1, S["steps"] + 1):
+        p = f"step{step}"
+        idx, noise = G[f"{p}/idx"], G[f"{p}/noise"]
+        for pol in pols:
+            _load_oracle_state(pol, L)
+        rec = orc.particle_train_step(L, S["buf"].gather(idx), noise)
+        outs = train_local(pols, rbs, b, indices=idx.reshape(n, b), noise=noise.reshape(n, b, -1), stats=True)
+        assert _rel_to_max(np.concatenate([o["y"] for o in outs]), rec["y"]) <= 1e-5, p
+        _check_replicas_equal(pols)
+        _params_close(pols[0].critic.numpy_dict(), L.critic, L.lr, (p, "critic"))
+        _params_close(pols[0].actor.numpy_dict(), L.actor, L.lr, (p, "actor"))
+        _params_close(pols[0].critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"))
+
+
+def test_local_replica_refuses_single_train():
+    from td3_amd import _lib
+    S = featured_setup("hc_layer")
+    pols, rbs = _replicas(S, 2, _make)
+    with pytest.raises(_lib.TD3Error, match="td3_train_step_local"):
+        pols[0].train(rbs[0], 64)
