@@ -128,7 +128,11 @@ typedef struct td3_config {
 
 enum td3_which {
   TD3_ACTOR = 0, TD3_ACTOR_TARGET = 1, TD3_CRITIC = 2, TD3_CRITIC_TARGET = 3,
-  TD3_ACTOR_ADAM_M = 4, TD3_ACTOR_ADAM_V = 5, TD3_CRITIC_ADAM_M = 6, TD3_CRITIC_ADAM_V = 7
+  TD3_ACTOR_ADAM_M = 4, TD3_ACTOR_ADAM_V = 5, TD3_CRITIC_ADAM_M = 6, TD3_CRITIC_ADAM_V = 7,
+  /* gradient arenas (read only): in data-parallel mode the all-reduced SUM of the replicas' batch-mean
+   * gradients of the last phase (divide by nranks for the mean); with weight normalization dL/dW.
+   * Not written by the single-device fused path (its dW tiles feed Adam directly). */
+  TD3_ACTOR_GRAD = 8, TD3_CRITIC_GRAD = 9
 };
 
 typedef struct td3_step_stats {   /* particles: y / q1 / q2 are [B][action_dim] */

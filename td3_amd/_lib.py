@@ -101,6 +101,7 @@ SIGNATURES = {
 
 TD3_ACTOR, TD3_ACTOR_TARGET, TD3_CRITIC, TD3_CRITIC_TARGET = 0, 1, 2, 3
 TD3_ACTOR_ADAM_M, TD3_ACTOR_ADAM_V, TD3_CRITIC_ADAM_M, TD3_CRITIC_ADAM_V = 4, 5, 6, 7
+TD3_ACTOR_GRAD, TD3_CRITIC_GRAD = 8, 9
 
 _lib = None
 _shutting_down = False

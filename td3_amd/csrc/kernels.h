@@ -221,6 +221,28 @@ struct DwArgs {
   int scaled;                     // 1: rows scaled by DwProb::rs (dw_kernel<true> / dw64_kernel<true>)
 };
 
+// Large batches (Bp a multiple of 64, Bp >= 512): the dW reduction over the batch rows split evenly
+// over a persistent grid of one workgroup per CU (dwsk_kernel), partial sums combined with the
+// optimizer update by a second launch (dwsk_combine_kernel).  A work unit is one 64-row step of one
+// tile: a 64x64 weight tile (dW = dZ^T U) or a 32-column vector tile (db, dgamma, dbeta); unit u is
+// step u % S of tile u / S (S = Bp / 64).  Virtual workgroup v (XCD-major: the 32 workgroups of an
+// XCD hold consecutive v, so an XCD streams one contiguous part of the tile list) takes units
+// [v*c, (v+1)*c) and writes one partial per tile it touched to slab[v][j] (j-th tile of its range).
+struct DwTile {
+  int prob;                       // DwArgs::probs index
+  int kind;                       // 0: 64x64 matrix tile (a = n tile, b = k tile), 1: vector tile (a = j)
+  int a, b;
+};
+struct DwSplit {
+  const DwTile* tiles; int ntile;
+  int S;                          // steps per tile (Bp / 64)
+  int c;                          // units per workgroup
+  int G;                          // workgroups (multiple of 8)
+  int J;                          // partial slots per workgroup
+  float* slab;                    // [G][J][4096]
+};
+int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s);
+
 // ------------------------------------------------------------------ launchers (kernels.hip)
 // launch_gemm's bump_actor: 0 bumps total_it / critic_step, 1 also actor_step, kBumpActorOnly only
 // actor_step (TD3_particles._actor_learn outside a train step: the actor's Adam step, no total_it)

@@ -2316,6 +2316,251 @@ __global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
   }
 }
 
+// ================================================================== split-K dW (kernels.h DwSplit)
+// Bp >= 512: the 64x64 tiles of dw64g_kernel did not fit the chip evenly -- Humanoid C_dw: 288 matrix
+// tiles + 74 vector tiles on 256 CUs, so 32 CUs ran two tiles back to back (50 us; one tile alone 23.5).
+// Here every tile's 64-row steps are cut into ONE list split evenly over one workgroup per CU; a
+// workgroup walks its share tile by tile (LDS-DMA staging as dw64g_kernel) and stores one fp32
+// partial per tile it touched; the combine launch sums a tile's partials in workgroup order (fixed
+// order: bitwise reproducible) and applies the optimizer.
+__device__ __forceinline__ int dwsk_virtual(int g, int G) { return (g & 7) * (G >> 3) + (g >> 3); }
+
+// Steps [s0, s1) of matrix tile (nt, kt) of P -> the 64x64 partial (row n - n0, column k - k0) at out.
+template <bool SC>
+__device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, int nt, int kt, int s0, int s1,
+                                            float* sm, float* out) {
+  float* const ssl = sm + 2 * 2 * 64 * 64;
+  const int n0 = nt * 64, k0 = kt * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
+  const int lr = lane >> 4, lc = (lane & 15) * 4;
+  int gcol[2], ucol[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * wave + 4 * j + lr;
+    const int c = lc ^ (((row >> 4) & 1) << 5);
+    gcol[j] = min(n0 + c, P.Np - 4);
+    ucol[j] = min(k0 + c, P.Kp - 4);
+  }
+  auto issue = [&](int st, int buf) {
+    float* g = sm + buf * 2 * 4096;
+    float* u = g + 4096;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rl = 8 * wave + 4 * j;
+      const size_t row = (size_t)(st * 64 + rl + lr);
+      glds16(P.G + row * P.ldg + gcol[j], g + rl * 64);
+      glds16(P.U + row * P.ldu + ucol[j], u + rl * 64);
+    }
+    if constexpr (SC) {
+      if (wave == 0) glds4(P.rs + (size_t)(st * 64 + lane) * P.ldrs, ssl + buf * 64);
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  issue(s0, 0);
+  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
+  const bool live = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
+  for (int st = s0; st < s1; ++st) {
+    const int buf = (st - s0) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step st has landed
+    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
+    if (st + 1 < s1) issue(st + 1, buf ^ 1);
+    if (!live) continue;
+    const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
+    const float* u = g + 4096;
+    float scl[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * q)
+                           : make_float4(1.f, 1.f, 1.f, 1.f);
+      scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const float ga = g[s2 * 64 + ca];
+      acc = mfma32x32x2(SC ? ga * scl[s2] : ga, u[s2 * 64 + cb], acc);
+    }
+  }
+  __syncthreads();                                   // staging buffers become the reduction tile
+  float* red = sm + (wave & 3) * 32 * 33;
+  if (rh == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[r];
+  }
+  __syncthreads();
+  if (rh == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      gst(out + (qn * 32 + mfma_row(r, lane)) * 64 + qk * 32 + i, acc[r] + red[mfma_row(r, lane) * 33 + i]);
+  }
+  __syncthreads();                                   // the next segment restages sm
+}
+
+// Steps [s0, s1) of vector tile j of P (32 columns): the partial db, dgamma, dbeta at out[0 / 32 / 64 + c].
+// Thread = 4 adjacent columns x one row of each 64-row step (64 row groups), 4 steps per load batch.
+template <bool SC>
+__device__ __forceinline__ void dwsk_vector(const DwArgs& a, const DwProb& P, int j, int s0, int s1, float* red,
+                                            float* out) {
+  constexpr int U = 4;
+  const int n0 = j * 32;
+  const int c4 = (threadIdx.x & 7) * 4, rg = threadIdx.x >> 3;
+  const bool ln = P.offg >= 0;
+  const bool hasb = P.offb >= 0;
+  const float* gzp = hasb ? P.G : P.GU;             // operands read from valid addresses, masked at use
+  const float* gup = ln ? P.GU : P.G;
+  const float* hp = ln ? P.H : P.G;
+  const float* stp = ln ? P.stats : P.G;
+  const int ldz = hasb ? P.ldg : P.ldgu, ldu = ln ? P.ldgu : P.ldg, ldh = ln ? P.ldh : P.ldg;
+  float sb[4] = {0.f, 0.f, 0.f, 0.f}, sg[4] = {0.f, 0.f, 0.f, 0.f}, sbeta[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int st = s0; st < s1; st += U) {
+    float4 gz[U], gu[U], hh[U];
+    float mu[U], rs[U], sc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = min(st + u, s1 - 1) * 64 + rg;  // clamped: loads stay unconditional
+      gz[u] = gld4(gzp + ((size_t)r * ldz + n0 + c4));
+      gu[u] = gld4(gup + ((size_t)r * ldu + n0 + c4));
+      hh[u] = gld4(hp + ((size_t)r * ldh + n0 + c4));
+      mu[u] = gld(stp + r);
+      rs[u] = gld(stp + (a.Bp + r));
+      sc[u] = SC ? gld(P.rs + (size_t)r * P.ldrs) : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (st + u >= s1) continue;
+      if (hasb) {
+        sb[0] += gz[u].x * sc[u]; sb[1] += gz[u].y * sc[u]; sb[2] += gz[u].z * sc[u]; sb[3] += gz[u].w * sc[u];
+      }
+      if (ln) {
+        const float g4[4] = {gu[u].x * sc[u], gu[u].y * sc[u], gu[u].z * sc[u], gu[u].w * sc[u]};
+        const float h4[4] = {hh[u].x, hh[u].y, hh[u].z, hh[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sg[e] += g4[e] * ((h4[e] - mu[u]) * rs[u]);
+          sbeta[e] += g4[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[(0 * 64 + rg) * 33 + c4 + e] = sb[e];
+    red[(1 * 64 + rg) * 33 + c4 + e] = sg[e];
+    red[(2 * 64 + rg) * 33 + c4 + e] = sbeta[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 96) {
+    const int w = threadIdx.x >> 5, c = threadIdx.x & 31;
+    float s = 0.f;
+#pragma unroll 8
+    for (int g = 0; g < 64; ++g) s += red[(w * 64 + g) * 33 + c];
+    gst(out + w * 32 + c, s);
+  }
+  __syncthreads();
+}
+
+template <bool SC>
+__global__ __launch_bounds__(512, 2) void dwsk_kernel(DwArgs a, DwSplit k) {
+  // ONE __shared__ object (a second one made hipcc drain the DMA before every step's first operand
+  // read, dw64g_kernel): [buf][operand][64 rows][64 cols (swizzled)], then SC's [buf][64] row scales
+  __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64];
+  const int v = dwsk_virtual((int)blockIdx.x, k.G);
+  TL_MARK(0);
+  const int64_t total = (int64_t)k.ntile * k.S;
+  int64_t u = (int64_t)v * k.c;
+  const int64_t u1 = u + k.c < total ? u + k.c : total;
+  int j = 0;
+  while (u < u1) {
+    const int t = __builtin_amdgcn_readfirstlane((int)(u / k.S));
+    const int s0 = (int)(u - (int64_t)t * k.S);
+    const int s1 = (int)((u1 - u) + s0 < k.S ? (u1 - u) + s0 : k.S);
+    const DwTile T = k.tiles[t];
+    const int pi = __builtin_amdgcn_readfirstlane(T.prob);
+    const DwProb& P = a.probs[pi];
+    float* out = k.slab + ((size_t)v * k.J + j) * 4096;
+    if (__builtin_amdgcn_readfirstlane(T.kind) == 0)
+      dwsk_matrix<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm,
+                      out);
+    else
+      dwsk_vector<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), s0, s1, sm, out);
+    u += s1 - s0;
+    ++j;
+  }
+  TL_MARK(3);
+}
+
+// One workgroup per tile: the tile's partials summed in workgroup order, then the optimizer (or the
+// gradient store of the data-parallel / weight-norm paths) on its elements.
+__global__ __launch_bounds__(256) void dwsk_combine_kernel(DwArgs a, DwSplit k) {
+  const int t = blockIdx.x;
+  const DwTile T = k.tiles[t];
+  const DwProb& P = a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
+  const int64_t ub = (int64_t)t * k.S;
+  const int v0 = (int)(ub / k.c), v1 = (int)((ub + k.S - 1) / k.c);
+  const AdamPw pw = adam_pw(a.adam);
+  auto part = [&](int v) -> const float* {
+    const int first = (int)((int64_t)v * k.c / k.S);
+    return k.slab + ((size_t)v * k.J + (t - first)) * 4096;
+  };
+  if (T.kind == 0) {
+    const int n0 = T.a * 64, k0 = T.b * 64;
+    const bool grad_only = a.mode == kDwGrad, pol = a.mode == kDwAdamPolyak;
+    const AdamK ak = make_adam(a.adam, pw);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e4 = q * 256 + threadIdx.x;            // float4 e4 of the 64x64 tile
+      const int row = e4 >> 4, col = (e4 & 15) * 4;
+      const int n = n0 + row, kk = k0 + col;
+      if (n >= P.Np || kk >= P.Kp) continue;         // Kp is a multiple of 32: whole float4 in or out
+      float4 g4 = gld4(part(v0) + row * 64 + col);
+      for (int v = v0 + 1; v <= v1; ++v) {
+        const float4 o = gld4(part(v) + row * 64 + col);
+        g4.x = g4.x + o.x; g4.y = g4.y + o.y; g4.z = g4.z + o.z; g4.w = g4.w + o.w;
+      }
+      const float gq[4] = {kk < P.kvalid ? g4.x : 0.f, kk + 1 < P.kvalid ? g4.y : 0.f,
+                           kk + 2 < P.kvalid ? g4.z : 0.f, kk + 3 < P.kvalid ? g4.w : 0.f};
+      const int64_t ix = P.offW + (int64_t)n * P.Kp + kk;
+      if (grad_only) {
+        gst4(a.adam.G + ix, make_float4(gq[0], gq[1], gq[2], gq[3]));
+        continue;
+      }
+      const float4 m4 = gld4(a.adam.M + ix), v4 = gld4(a.adam.V + ix), p4 = gld4(a.adam.P + ix);
+      const float4 t4 = gld4((pol ? a.adam.T : a.adam.P) + ix);
+      float mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+      float pp[4] = {p4.x, p4.y, p4.z, p4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {                   // torch _single_tensor_adam, as adam_elem
+        mm[e] = __fmaf_rn(ak.w1, gq[e] - mm[e], mm[e]);
+        vv[e] = vv[e] * ak.b2;
+        vv[e] = vv[e] + (ak.c2 * gq[e]) * gq[e];
+        const float denom = sqrtf(vv[e]) / ak.bc2s + ak.eps;
+        pp[e] = pp[e] + (ak.negss * mm[e]) / denom;
+        tt[e] = ak.tau * pp[e] + ak.omt * tt[e];
+      }
+      gst4(a.adam.M + ix, make_float4(mm[0], mm[1], mm[2], mm[3]));
+      gst4(a.adam.V + ix, make_float4(vv[0], vv[1], vv[2], vv[3]));
+      gst4(a.adam.P + ix, make_float4(pp[0], pp[1], pp[2], pp[3]));
+      if (pol) gst4(a.adam.T + ix, make_float4(tt[0], tt[1], tt[2], tt[3]));
+    }
+    return;
+  }
+  if (threadIdx.x >= 32) return;
+  const int c = threadIdx.x, n0 = T.a * 32;
+  float gq[3];
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    float s = gld(part(v0) + w * 32 + c);
+    for (int v = v0 + 1; v <= v1; ++v) s = s + gld(part(v) + w * 32 + c);
+    gq[w] = s;
+  }
+  const bool ln = P.offg >= 0, hasb = P.offb >= 0;
+  const int64_t idx[3] = {P.offb + n0 + c, P.offg + n0 + c, P.offbeta + n0 + c};
+  const bool ok[3] = {hasb, ln, ln};
+  apply_grads<3>(a, make_adam(a.adam, pw), idx, gq, ok);
+}
+
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, int polyak) {
   const AdamK k = make_adam(a);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -2678,6 +2923,19 @@ int launch_dw(const DwArgs& a, int nblocks, hipStream_t s) {
     if (a.scaled) hipLaunchKernelGGL(dw_kernel<true>, grid, dim3(256), 0, s, a, nblocks);
     else hipLaunchKernelGGL(dw_kernel<false>, grid, dim3(256), 0, s, a, nblocks);
   }
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
+  if (k.ntile <= 0) return 0;
+  if (k.G <= 0 || (k.G & 7) || k.S <= 0 || k.c <= 0 || (a.Bp & 63) || a.Bp != 64 * k.S) {
+    set_error("launch_dw_split: bad split (G %d, S %d, c %d, Bp %d)", k.G, k.S, k.c, a.Bp);
+    return -1;
+  }
+  if (a.scaled) hipLaunchKernelGGL(dwsk_kernel<true>, dim3(k.G), dim3(512), 0, s, a, k);
+  else hipLaunchKernelGGL(dwsk_kernel<false>, dim3(k.G), dim3(512), 0, s, a, k);
+  hipLaunchKernelGGL(dwsk_combine_kernel, dim3(k.ntile), dim3(256), 0, s, a, k);
   TD3_HIP(hipGetLastError());
   return 0;
 }

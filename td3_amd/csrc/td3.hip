@@ -756,6 +756,13 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
   return 0;
 }
 
+// B >= 512 with Bp a multiple of 64: the split-K persistent dW (dwsk_kernel + dwsk_combine_kernel)
+// instead of one 64x64 tile per workgroup (dw64g_kernel)
+#ifndef TD3_DWSK
+#define TD3_DWSK 1
+#endif
+constexpr int kDwSplitWorkgroups = 256;   // one per CU of the MI355X
+
 // Weight / bias / LN grads of every layer of `items`, fused with the optimizer.
 // enc (TD3_particles): the encoder partial slabs of `items` (reduced + optimizer in one launch).
 // unit_scale (featured critic): per item, the dense [Bp] row scale g_r of its unit-gradient
@@ -852,8 +859,41 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.mode = (dp || wn) ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
   a.tile64 = tile64 ? 1 : 0;
   a.scaled = unit_scale ? 1 : 0;
-  st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
-                std::string(tile64 ? "td3::dw64_kernel<" : "td3::dw_kernel<") + (unit_scale ? "true>" : "false>")});
+  if (tile64 && Bp % 64 == 0 && TD3_DWSK) {
+    // split-K persistent path (kernels.h DwSplit): every tile's 64-row steps in one list, cut evenly
+    // over one workgroup per CU; per problem its 64x64 matrix tiles (n tile major, so an XCD's
+    // consecutive tiles share dZ column blocks), then its 32-column vector tiles
+    std::vector<DwTile> tiles;
+    for (int pi = 0; pi < a.nprob; ++pi) {
+      const DwProb& p = a.probs[pi];
+      const int ntn = (p.Np + 63) / 64;
+      for (int nt = 0; nt < ntn && p.ntk > 0; ++nt)
+        for (int kt = 0; kt < p.ntk; ++kt) tiles.push_back(DwTile{pi, 0, nt, kt});
+      for (int j = 0; j < p.Np / 32; ++j) tiles.push_back(DwTile{pi, 1, j, 0});
+    }
+    DwSplit k{};
+    k.ntile = (int)tiles.size();
+    k.S = Bp / 64;
+    k.G = kDwSplitWorkgroups;
+    const int64_t units = (int64_t)k.ntile * k.S;
+    k.c = (int)((units + k.G - 1) / k.G);
+    for (int v = 0; v < k.G; ++v) {               // partial slots: the tiles one workgroup's units touch
+      const int64_t u0 = (int64_t)v * k.c, u1 = std::min<int64_t>(units, u0 + k.c);
+      if (u0 < u1) k.J = std::max(k.J, (int)((u1 - 1) / k.S - u0 / k.S + 1));
+    }
+    void* d = nullptr;
+    TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
+    k.tiles = static_cast<const DwTile*>(d);
+    void* slab = nullptr;
+    TD3_HIP(hipMalloc(&slab, (size_t)k.G * k.J * 4096 * sizeof(float)));
+    owned.push_back(slab);
+    k.slab = static_cast<float*>(slab);
+    st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw_split(a, k, s); }, flops,
+                  std::string("td3::dwsk_kernel<") + (unit_scale ? "true>" : "false>")});
+  } else {
+    st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
+                  std::string(tile64 ? "td3::dw64_kernel<" : "td3::dw_kernel<") + (unit_scale ? "true>" : "false>")});
+  }
   if (enc_nwg > 0) {
     EncAdamArgs ea{};
     for (auto& it : items) {
@@ -2346,6 +2386,8 @@ static int which_ptr(td3_handle* h, int which, Group** g, float** base) {
     case TD3_ACTOR_ADAM_V: *g = &h->actor; *base = h->actor.V; return 0;
     case TD3_CRITIC_ADAM_M: *g = &h->critic; *base = h->critic.M; return 0;
     case TD3_CRITIC_ADAM_V: *g = &h->critic; *base = h->critic.V; return 0;
+    case TD3_ACTOR_GRAD: *g = &h->actor; *base = h->actor.G; return 0;
+    case TD3_CRITIC_GRAD: *g = &h->critic; *base = h->critic.G; return 0;
   }
   set_error("unknown tensor group %d", which);
   return -1;
@@ -2378,6 +2420,7 @@ int td3_get_params(td3_handle* h, int which, float* out, int64_t n) {
 
 int td3_set_params(td3_handle* h, int which, const float* in, int64_t n) {
   TD3_ARG(h && in, "null argument");
+  TD3_ARG(which != TD3_ACTOR_GRAD && which != TD3_CRITIC_GRAD, "the gradient arenas are read only");
   Group* g;
   float* base;
   TD3_RC(which_ptr(h, which, &g, &base));

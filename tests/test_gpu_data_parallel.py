@@ -8,9 +8,13 @@ over the replicas' gradient arenas.  Replica k samples its own ring at rows
 
 Checks, per step (teacher-forced from the oracle's state):
 * the replicas end bit-identical (actor, critic, targets, Adam moments);
-* they equal the oracle's ONE step on the concatenated global batch (SURVEY §8e equivalence:
-  the losses are batch means, so the mean of the shard gradients is the global gradient), at the
-  SURVEY §8c tolerances.
+* the all-reduced gradient (the G arena: sum over replicas; / n = mean of the shard gradients)
+  equals the oracle's gradient of the ONE global-batch loss (SURVEY §8e equivalence: the losses
+  are batch means) at the SURVEY §8c gradient tolerance;
+* the post-Adam parameters equal the oracle's global-batch step within 2*lr everywhere and within
+  1e-6 + 1e-5|x| on >= 99 % of the elements.  (The single-device tests hold 99.9 %: here the
+  gradient is a different fp32 summation -- two shard sums added -- and Adam's m / sqrt(v) turns
+  the rounding of near-zero gradients into up to lr-sized moves of a few more elements.)
 """
 import numpy as np
 import pytest
@@ -37,6 +41,27 @@ def _all_views(pol):
     from td3_amd.TD3_featured import _ParamView
     return [pol.actor.flat(), pol.critic.flat(), pol.actor_target.flat(), pol.critic_target.flat(),
             _ParamView(pol, _lib.TD3_ACTOR_ADAM_M, 0).flat(), _ParamView(pol, _lib.TD3_CRITIC_ADAM_V, 1).flat()]
+
+
+def _check_grads(pol, n, rec, what):
+    """All-reduced gradients / n vs the oracle's global-batch gradients, per tensor relative to its
+    largest element (as tests/test_oracle_golden.py).  The critic gradient comes from exactly the
+    oracle's state: SURVEY §8c's gradient tolerance (2e-4 of the tensor's scale).  The actor gradient
+    is taken through the critic AFTER this step's update, which agrees with the oracle's only within
+    the post-Adam contract (near-zero gradients flip sign: up to 2*lr per element), and a moved critic
+    weight can flip a ReLU of Q1 on a row: 1e-2 of the tensor's scale.  Weight-normalised Linears keep
+    dL/dW in the arena (wn_kernel forms dg / dv in registers): their biases are compared."""
+    from td3_amd import _lib
+    from td3_amd.TD3_featured import _ParamView
+    groups = [("critic", _lib.TD3_CRITIC_GRAD, 1, rec["critic_grads"], 2e-4)]
+    if "actor_grads" in rec:
+        groups.append(("actor", _lib.TD3_ACTOR_GRAD, 0, rec["actor_grads"], 1e-2))
+    for name, which, g, ref, tol in groups:
+        got = _ParamView(pol, which, g).numpy_dict()
+        for k, v in ref.items():
+            if k.endswith(("weight_g", "weight_v")):
+                continue
+            assert _rel_to_max(got[k] / n, v) <= tol, (what, name, k, _rel_to_max(got[k] / n, v))
 
 
 def _check_replicas_equal(pols):
@@ -74,10 +99,11 @@ def test_local_replicas_equal_global_batch_step(name, n):
                                        rtol=1e-5, atol=1e-7)
         _check_replicas_equal(pols)
         pol = pols[0]
-        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (p, "critic"))
-        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"))
-        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (p, "actor"))
-        _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"))
+        _check_grads(pol, n, rec, p)
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (p, "critic"), frac=0.99)
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"), frac=0.99)
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (p, "actor"), frac=0.99)
+        _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"), frac=0.99)
         assert all(q._counters() == (L.total_it, L.critic_step, L.actor_step) for q in pols)
 
 
@@ -119,9 +145,10 @@ def test_particle_local_replicas_equal_global_batch_step():
         outs = train_local(pols, rbs, b, indices=idx.reshape(n, b), noise=noise.reshape(n, b, -1), stats=True)
         assert _rel_to_max(np.concatenate([o["y"] for o in outs]), rec["y"]) <= 1e-5, p
         _check_replicas_equal(pols)
-        _params_close(pols[0].critic.numpy_dict(), L.critic, L.lr, (p, "critic"))
-        _params_close(pols[0].actor.numpy_dict(), L.actor, L.lr, (p, "actor"))
-        _params_close(pols[0].critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"))
+        _check_grads(pols[0], n, rec, p)
+        _params_close(pols[0].critic.numpy_dict(), L.critic, L.lr, (p, "critic"), frac=0.99)
+        _params_close(pols[0].actor.numpy_dict(), L.actor, L.lr, (p, "actor"), frac=0.99)
+        _params_close(pols[0].critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"), frac=0.99)
 
 
 def test_local_replica_refuses_single_train():

@@ -37,13 +37,17 @@ def _make(S, use_graph=True):
     return pol, rb
 
 
-def _params_close(gpu, ref, lr, what):
+def _params_close(gpu, ref, lr, what, frac=0.999):
+    """SURVEY §8c post-Adam contract: within 1e-6 + 1e-5|x| on >= `frac` of the elements, and within
+    2*lr everywhere -- the update of a near-zero gradient whose sign flips between two fp32
+    summation orders is +-lr*m/denom ~ +-lr, so the two parameters differ by up to 2*lr (the 0.1 %
+    allows for fp32 rounding on top of that bound)."""
     for k in ref:
         g, o = np.asarray(gpu[k], np.float64), np.asarray(ref[k], np.float64)
         err = np.abs(g - o)
         tight = err <= 1e-6 + 1e-5 * np.abs(o)
-        assert tight.mean() >= 0.999 or (~tight).sum() <= 2, (what, k, (~tight).sum(), err.max())
-        assert err.max() <= 2.5 * lr, (what, k, err.max())
+        assert tight.mean() >= frac or (~tight).sum() <= 2, (what, k, (~tight).sum(), err.max())
+        assert err.max() <= 2 * lr * 1.001, (what, k, err.max())
 
 
 def _load_oracle_state(pol, L):
