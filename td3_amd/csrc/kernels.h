@@ -224,22 +224,28 @@ struct DwArgs {
 // Large batches (Bp a multiple of 64, Bp >= 512): the dW reduction over the batch rows split evenly
 // over a persistent grid of one workgroup per CU (dwsk_kernel), partial sums combined with the
 // optimizer update by a second launch (dwsk_combine_kernel).  A work unit is one 64-row step of one
-// tile: a 64x64 weight tile (dW = dZ^T U) or a 32-column vector tile (db, dgamma, dbeta); unit u is
-// step u % S of tile u / S (S = Bp / 64).  Virtual workgroup v (XCD-major: the 32 workgroups of an
-// XCD hold consecutive v, so an XCD streams one contiguous part of the tile list) takes units
-// [v*c, (v+1)*c) and writes one partial per tile it touched to slab[v][j] (j-th tile of its range).
+// tile: a tm x tm weight tile (dW = dZ^T U) or a 32-column vector tile (db, dgamma, dbeta); unit u is
+// step u % S of tile u / S (S = Bp / 64).  Units carry a cost weight (a matrix step costs several
+// vector steps) and the host cuts the weighted list into G contiguous ranges: virtual workgroup v
+// (XCD-major: the G/8 workgroups of an XCD hold consecutive v, so an XCD streams one contiguous part
+// of the tile list) takes units [wg_unit[v], wg_unit[v+1]) and writes one partial per tile it
+// touched to slab[v][j] (j-th tile of its range); tile t's partials come from workgroups
+// tile_wg[2t] .. tile_wg[2t+1] (empty ranges skipped).
 struct DwTile {
   int prob;                       // DwArgs::probs index
-  int kind;                       // 0: 64x64 matrix tile (a = n tile, b = k tile), 1: vector tile (a = j)
+  int kind;                       // 0: tm x tm matrix tile (a = n tile, b = k tile), 1: vector tile (a = j)
   int a, b;
 };
 struct DwSplit {
   const DwTile* tiles; int ntile;
   int S;                          // steps per tile (Bp / 64)
-  int c;                          // units per workgroup
   int G;                          // workgroups (multiple of 8)
   int J;                          // partial slots per workgroup
-  float* slab;                    // [G][J][4096]
+  int tm;                         // matrix tile edge: 64 or 128
+  int slot;                       // floats per partial slot (tm * tm)
+  const int* wg_unit;             // [G + 1]
+  const int* tile_wg;             // [ntile][2]
+  float* slab;                    // [G][J][slot]
 };
 int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s);
 

@@ -2317,12 +2317,14 @@ __global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
 }
 
 // ================================================================== split-K dW (kernels.h DwSplit)
-// Bp >= 512: the 64x64 tiles of dw64g_kernel did not fit the chip evenly -- Humanoid C_dw: 288 matrix
-// tiles + 74 vector tiles on 256 CUs, so 32 CUs ran two tiles back to back (50 us; one tile alone 23.5).
-// Here every tile's 64-row steps are cut into ONE list split evenly over one workgroup per CU; a
-// workgroup walks its share tile by tile (LDS-DMA staging as dw64g_kernel) and stores one fp32
-// partial per tile it touched; the combine launch sums a tile's partials in workgroup order (fixed
-// order: bitwise reproducible) and applies the optimizer.
+// Bp >= 512: one tile per workgroup (dw64g_kernel) did not fit the chip evenly -- Humanoid C_dw: 288
+// 64x64 matrix tiles + 74 vector tiles on 256 CUs, so 32 CUs ran two tiles back to back (50 us; one
+// tile alone 23.5).  Here every tile's 64-row steps are cut into ONE weighted list split evenly over
+// one workgroup per CU; a workgroup walks its share tile by tile (LDS-DMA staging as dw64g_kernel)
+// and stores one fp32 partial per tile it touched; the combine launch sums a tile's partials in
+// workgroup order (fixed order: bitwise reproducible) and applies the optimizer.  Matrix tiles are
+// 128 x 128 by default (dwsk_matrix128: 64 KB staged per step for 64 MFMA per wave -- a 64 x 64 step
+// stages 32 KB for 16, and was bound by its DMA round trip, not the MFMA pipe).
 __device__ __forceinline__ int dwsk_virtual(int g, int G) { return (g & 7) * (G >> 3) + (g >> 3); }
 
 // Steps [s0, s1) of matrix tile (nt, kt) of P -> the 64x64 partial (row n - n0, column k - k0) at out.
@@ -2398,6 +2400,102 @@ __device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, in
   __syncthreads();                                   // the next segment restages sm
 }
 
+// Steps [s0, s1) of 128 x 128 matrix tile (nt, kt) of P -> the partial (row n - n0, column k - k0,
+// ld 128) at out; quadrants past Np / Kp are neither fetched, multiplied nor stored.  LDS per buffer
+// and operand: [64 rows][128 cols], the 32-column groups 2c and 2c+1 swapped on rows with bit 4 set
+// (an MFMA operand read takes rows 16 apart in its two lane halves, which then hit other banks).
+// Wave w: n quadrant w >> 1 and k quadrants (w & 1), (w & 1) + 2, so the two waves of a SIMD (w, w + 4)
+// own n quadrants {a, a + 2} x k quadrants {b, b + 2}: an edge tile's live quadrants stay spread
+// over the four SIMDs.
+template <bool SC>
+__device__ __forceinline__ void dwsk_matrix128(const DwArgs& a, const DwProb& P, int nt, int kt, int s0, int s1,
+                                               float* sm, float* out) {
+  float* const ssl = sm + 2 * 2 * 64 * 128;
+  const int n0 = nt * 128, k0 = kt * 128;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+  const int qn = wave >> 1, qk0 = wave & 1, qk1 = qk0 + 2;
+  // DMA lanes: wave w fills rows 8w .. 8w+7 of both operands (four 2-row wave-instructions each);
+  // lane L -> row 8w + 2j + L/32, LDS columns 4(L&31) .. +3 <- source columns of the swizzle
+  const int lr = lane >> 5, lc = (lane & 31) * 4;
+  int gcol[4], ucol[4];
+  bool gl[4], ul[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * wave + 2 * j + lr;
+    const int c = lc ^ (((row >> 4) & 1) << 5);
+    gcol[j] = n0 + c;
+    ucol[j] = k0 + c;
+    gl[j] = gcol[j] < P.Np;                          // Np, Kp multiples of 32: whole column groups
+    ul[j] = ucol[j] < P.Kp;
+  }
+  auto issue = [&](int st, int buf) {
+    float* g = sm + buf * 2 * 8192;
+    float* u = g + 8192;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int rl = 8 * wave + 2 * j;
+      const size_t row = (size_t)(st * 64 + rl + lr);
+      if (gl[j]) glds16(P.G + row * P.ldg + gcol[j], g + rl * 128);
+      if (ul[j]) glds16(P.U + row * P.ldu + ucol[j], u + rl * 128);
+    }
+    if constexpr (SC) {
+      if (wave == 0) glds4(P.rs + (size_t)(st * 64 + lane) * P.ldrs, ssl + buf * 64);
+    }
+  };
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = 0.f;
+    acc1[r] = 0.f;
+  }
+  issue(s0, 0);
+  const int ca = (qn ^ h) * 32 + i, cb0 = (qk0 ^ h) * 32 + i, cb1 = (qk1 ^ h) * 32 + i;
+  const bool live_n = n0 + qn * 32 < P.Np;
+  const bool live0 = live_n && k0 + qk0 * 32 < P.Kp, live1 = live_n && k0 + qk1 * 32 < P.Kp;
+  for (int st = s0; st < s1; ++st) {
+    const int buf = (st - s0) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step st has landed
+    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
+    if (st + 1 < s1) issue(st + 1, buf ^ 1);
+    if (!live0) continue;
+    // MFMA s (0..31) takes rows 32 (s >> 4) + 16 h + (s & 15): lane half h's rows have bit 4 = h
+    const float* g = sm + buf * 2 * 8192 + 16 * h * 128;
+    const float* u = g + 8192;
+    float scl[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + 32 * (q >> 2) + 16 * h + 4 * (q & 3))
+                           : make_float4(1.f, 1.f, 1.f, 1.f);
+      scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
+    }
+    if (live1) {
+#pragma unroll
+      for (int s2 = 0; s2 < 32; ++s2) {
+        const int r = 32 * (s2 >> 4) + (s2 & 15);
+        const float ga = SC ? g[r * 128 + ca] * scl[s2] : g[r * 128 + ca];
+        acc0 = mfma32x32x2(ga, u[r * 128 + cb0], acc0);
+        acc1 = mfma32x32x2(ga, u[r * 128 + cb1], acc1);
+      }
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 32; ++s2) {
+        const int r = 32 * (s2 >> 4) + (s2 & 15);
+        const float ga = SC ? g[r * 128 + ca] * scl[s2] : g[r * 128 + ca];
+        acc0 = mfma32x32x2(ga, u[r * 128 + cb0], acc0);
+      }
+    }
+  }
+  if (live0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gst(out + (qn * 32 + mfma_row(r, lane)) * 128 + qk0 * 32 + i, acc0[r]);
+  }
+  if (live1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gst(out + (qn * 32 + mfma_row(r, lane)) * 128 + qk1 * 32 + i, acc1[r]);
+  }
+  __syncthreads();                                   // the next segment restages sm
+}
+
 // Steps [s0, s1) of vector tile j of P (32 columns): the partial db, dgamma, dbeta at out[0 / 32 / 64 + c].
 // Thread = 4 adjacent columns x one row of each 64-row step (64 row groups), 4 steps per load batch.
 template <bool SC>
@@ -2461,62 +2559,65 @@ __device__ __forceinline__ void dwsk_vector(const DwArgs& a, const DwProb& P, in
   __syncthreads();
 }
 
-template <bool SC>
-__global__ __launch_bounds__(512, 2) void dwsk_kernel(DwArgs a, DwSplit k) {
+template <bool SC, bool T128>
+__global__ __launch_bounds__(512, T128 ? 1 : 2) void dwsk_kernel(DwArgs a, DwSplit k) {
   // ONE __shared__ object (a second one made hipcc drain the DMA before every step's first operand
-  // read, dw64g_kernel): [buf][operand][64 rows][64 cols (swizzled)], then SC's [buf][64] row scales
-  __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64];
+  // read, dw64g_kernel): [buf][operand][64 rows][tm cols (swizzled)], then SC's [buf][64] row scales
+  __shared__ float sm[2 * 2 * 64 * (T128 ? 128 : 64) + 2 * 64];
   const int v = dwsk_virtual((int)blockIdx.x, k.G);
   TL_MARK(0);
-  const int64_t total = (int64_t)k.ntile * k.S;
-  int64_t u = (int64_t)v * k.c;
-  const int64_t u1 = u + k.c < total ? u + k.c : total;
+  int u = k.wg_unit[v];
+  const int u1 = k.wg_unit[v + 1];
   int j = 0;
   while (u < u1) {
-    const int t = __builtin_amdgcn_readfirstlane((int)(u / k.S));
-    const int s0 = (int)(u - (int64_t)t * k.S);
-    const int s1 = (int)((u1 - u) + s0 < k.S ? (u1 - u) + s0 : k.S);
+    const int t = __builtin_amdgcn_readfirstlane(u / k.S);
+    const int s0 = u - t * k.S;
+    const int s1 = (u1 - u) + s0 < k.S ? (u1 - u) + s0 : k.S;
     const DwTile T = k.tiles[t];
     const int pi = __builtin_amdgcn_readfirstlane(T.prob);
     const DwProb& P = a.probs[pi];
-    float* out = k.slab + ((size_t)v * k.J + j) * 4096;
-    if (__builtin_amdgcn_readfirstlane(T.kind) == 0)
-      dwsk_matrix<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm,
-                      out);
-    else
-      dwsk_vector<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), s0, s1, sm, out);
+    float* out = k.slab + ((size_t)v * k.J + j) * k.slot;
+    const int ta = __builtin_amdgcn_readfirstlane(T.a);
+    if (__builtin_amdgcn_readfirstlane(T.kind) == 0) {
+      if constexpr (T128) dwsk_matrix128<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
+      else dwsk_matrix<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
+    } else {
+      dwsk_vector<SC>(a, P, ta, s0, s1, sm, out);
+    }
     u += s1 - s0;
     ++j;
   }
   TL_MARK(3);
 }
 
-// One workgroup per tile: the tile's partials summed in workgroup order, then the optimizer (or the
-// gradient store of the data-parallel / weight-norm paths) on its elements.
+// Four workgroups per tile (a quarter of a matrix tile's rows each; a vector tile uses the first):
+// the tile's partials summed in workgroup order, then the optimizer (or the gradient store of the
+// data-parallel / weight-norm paths) on its elements.
 __global__ __launch_bounds__(256) void dwsk_combine_kernel(DwArgs a, DwSplit k) {
-  const int t = blockIdx.x;
+  const int t = blockIdx.x >> 2, qtr = blockIdx.x & 3;
   const DwTile T = k.tiles[t];
   const DwProb& P = a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
-  const int64_t ub = (int64_t)t * k.S;
-  const int v0 = (int)(ub / k.c), v1 = (int)((ub + k.S - 1) / k.c);
+  const int v0 = k.tile_wg[2 * t], v1 = k.tile_wg[2 * t + 1];
   const AdamPw pw = adam_pw(a.adam);
   auto part = [&](int v) -> const float* {
-    const int first = (int)((int64_t)v * k.c / k.S);
-    return k.slab + ((size_t)v * k.J + (t - first)) * 4096;
+    return k.slab + ((size_t)v * k.J + (t - k.wg_unit[v] / k.S)) * k.slot;
   };
+  auto live = [&](int v) { return k.wg_unit[v] < k.wg_unit[v + 1]; };
   if (T.kind == 0) {
-    const int n0 = T.a * 64, k0 = T.b * 64;
+    const int tm = k.tm, c4 = tm >> 2;                // float4s per partial row
+    const int n0 = T.a * tm, k0 = T.b * tm;
+    const int per = tm * tm / (16 * 256);             // float4s per thread in a quarter: 1 or 4
     const bool grad_only = a.mode == kDwGrad, pol = a.mode == kDwAdamPolyak;
     const AdamK ak = make_adam(a.adam, pw);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e4 = q * 256 + threadIdx.x;            // float4 e4 of the 64x64 tile
-      const int row = e4 >> 4, col = (e4 & 15) * 4;
+    for (int q = 0; q < per; ++q) {
+      const int e4 = (qtr * per + q) * 256 + threadIdx.x;
+      const int row = e4 / c4, col = (e4 % c4) * 4;
       const int n = n0 + row, kk = k0 + col;
       if (n >= P.Np || kk >= P.Kp) continue;         // Kp is a multiple of 32: whole float4 in or out
-      float4 g4 = gld4(part(v0) + row * 64 + col);
+      float4 g4 = gld4(part(v0) + row * tm + col);
       for (int v = v0 + 1; v <= v1; ++v) {
-        const float4 o = gld4(part(v) + row * 64 + col);
+        if (!live(v)) continue;
+        const float4 o = gld4(part(v) + row * tm + col);
         g4.x = g4.x + o.x; g4.y = g4.y + o.y; g4.z = g4.z + o.z; g4.w = g4.w + o.w;
       }
       const float gq[4] = {kk < P.kvalid ? g4.x : 0.f, kk + 1 < P.kvalid ? g4.y : 0.f,
@@ -2546,13 +2647,14 @@ __global__ __launch_bounds__(256) void dwsk_combine_kernel(DwArgs a, DwSplit k) 
     }
     return;
   }
-  if (threadIdx.x >= 32) return;
+  if (qtr != 0 || threadIdx.x >= 32) return;
   const int c = threadIdx.x, n0 = T.a * 32;
   float gq[3];
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
     float s = gld(part(v0) + w * 32 + c);
-    for (int v = v0 + 1; v <= v1; ++v) s = s + gld(part(v) + w * 32 + c);
+    for (int v = v0 + 1; v <= v1; ++v)
+      if (live(v)) s = s + gld(part(v) + w * 32 + c);
     gq[w] = s;
   }
   const bool ln = P.offg >= 0, hasb = P.offb >= 0;
@@ -2929,13 +3031,20 @@ int launch_dw(const DwArgs& a, int nblocks, hipStream_t s) {
 
 int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
   if (k.ntile <= 0) return 0;
-  if (k.G <= 0 || (k.G & 7) || k.S <= 0 || k.c <= 0 || (a.Bp & 63) || a.Bp != 64 * k.S) {
-    set_error("launch_dw_split: bad split (G %d, S %d, c %d, Bp %d)", k.G, k.S, k.c, a.Bp);
+  if (k.G <= 0 || (k.G & 7) || k.S <= 0 || (a.Bp & 63) || a.Bp != 64 * k.S || (k.tm != 64 && k.tm != 128) ||
+      k.slot < k.tm * k.tm || k.J <= 0) {
+    set_error("launch_dw_split: bad split (G %d, S %d, tm %d, slot %d, J %d, Bp %d)", k.G, k.S, k.tm, k.slot,
+              k.J, a.Bp);
     return -1;
   }
-  if (a.scaled) hipLaunchKernelGGL(dwsk_kernel<true>, dim3(k.G), dim3(512), 0, s, a, k);
-  else hipLaunchKernelGGL(dwsk_kernel<false>, dim3(k.G), dim3(512), 0, s, a, k);
-  hipLaunchKernelGGL(dwsk_combine_kernel, dim3(k.ntile), dim3(256), 0, s, a, k);
+  if (k.tm == 128) {
+    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, true>), dim3(k.G), dim3(512), 0, s, a, k);
+    else hipLaunchKernelGGL((dwsk_kernel<false, true>), dim3(k.G), dim3(512), 0, s, a, k);
+  } else {
+    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false>), dim3(k.G), dim3(512), 0, s, a, k);
+    else hipLaunchKernelGGL((dwsk_kernel<false, false>), dim3(k.G), dim3(512), 0, s, a, k);
+  }
+  hipLaunchKernelGGL(dwsk_combine_kernel, dim3(4 * k.ntile), dim3(256), 0, s, a, k);
   TD3_HIP(hipGetLastError());
   return 0;
 }

@@ -19,7 +19,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <functional>
 #include <map>
 #include <memory>
@@ -761,7 +763,18 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 #ifndef TD3_DWSK
 #define TD3_DWSK 1
 #endif
-constexpr int kDwSplitWorkgroups = 256;   // one per CU of the MI355X
+#ifndef TD3_DWSK_G
+#define TD3_DWSK_G 256
+#endif
+constexpr int kDwSplitWorkgroups = TD3_DWSK_G;   // one per CU of the MI355X
+// Matrix tile edge (128; TD3_DWSK_T=64 selects dw64g-sized tiles) and the cost of a full matrix
+// step relative to a vector step (TD3_DWSK_WM, default 8): read when a plan is built, for A/B runs
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atoi(e) : dflt;
+}
+static int dwsk_tile_edge() { return env_int("TD3_DWSK_T", 128) == 64 ? 64 : 128; }
+static int dwsk_matrix_weight() { return std::max(1, env_int("TD3_DWSK_WM", 8)); }
 
 // Weight / bias / LN grads of every layer of `items`, fused with the optimizer.
 // enc (TD3_particles): the encoder partial slabs of `items` (reduced + optimizer in one launch).
@@ -860,36 +873,72 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.tile64 = tile64 ? 1 : 0;
   a.scaled = unit_scale ? 1 : 0;
   if (tile64 && Bp % 64 == 0 && TD3_DWSK) {
-    // split-K persistent path (kernels.h DwSplit): every tile's 64-row steps in one list, cut evenly
-    // over one workgroup per CU; per problem its 64x64 matrix tiles (n tile major, so an XCD's
-    // consecutive tiles share dZ column blocks), then its 32-column vector tiles
+    // split-K persistent path (kernels.h DwSplit): every tile's 64-row steps in one weighted list,
+    // cut evenly over one workgroup per CU; per problem its tm x tm matrix tiles (n tile major, so an
+    // XCD's consecutive tiles share dZ column blocks), then its 32-column vector tiles
+    const int tm = dwsk_tile_edge();
+    const int wm = dwsk_matrix_weight();
     std::vector<DwTile> tiles;
+    std::vector<int> wt;                          // cost of one 64-row step of the tile
     for (int pi = 0; pi < a.nprob; ++pi) {
       const DwProb& p = a.probs[pi];
-      const int ntn = (p.Np + 63) / 64;
-      for (int nt = 0; nt < ntn && p.ntk > 0; ++nt)
-        for (int kt = 0; kt < p.ntk; ++kt) tiles.push_back(DwTile{pi, 0, nt, kt});
-      for (int j = 0; j < p.Np / 32; ++j) tiles.push_back(DwTile{pi, 1, j, 0});
+      if (p.ntk > 0) {
+        for (int nt = 0; nt < (p.Np + tm - 1) / tm; ++nt)
+          for (int kt = 0; kt < (p.Kp + tm - 1) / tm; ++kt) {
+            tiles.push_back(DwTile{pi, 0, nt, kt});
+            // MFMA work of the busiest SIMD (dwsk_matrix128's quadrant map), out of 4 quadrants
+            const int an = std::min(tm, p.Np - nt * tm) / 32, ak = std::min(tm, p.Kp - kt * tm) / 32;
+            const int q = tm == 128 ? (an > 2 ? 2 : 1) * (ak > 2 ? 2 : 1) : 1;
+            wt.push_back(2 + wm * q / 4);
+          }
+      }
+      for (int j = 0; j < p.Np / 32; ++j) {
+        tiles.push_back(DwTile{pi, 1, j, 0});
+        wt.push_back(1);
+      }
     }
     DwSplit k{};
     k.ntile = (int)tiles.size();
     k.S = Bp / 64;
     k.G = kDwSplitWorkgroups;
-    const int64_t units = (int64_t)k.ntile * k.S;
-    k.c = (int)((units + k.G - 1) / k.G);
-    for (int v = 0; v < k.G; ++v) {               // partial slots: the tiles one workgroup's units touch
-      const int64_t u0 = (int64_t)v * k.c, u1 = std::min<int64_t>(units, u0 + k.c);
-      if (u0 < u1) k.J = std::max(k.J, (int)((u1 - 1) / k.S - u0 / k.S + 1));
+    k.tm = tm;
+    k.slot = tm * tm;
+    const int units = k.ntile * k.S;
+    int64_t wtot = 0;
+    for (int w : wt) wtot += (int64_t)w * k.S;
+    const int64_t cw = (wtot + k.G - 1) / k.G;
+    // unit -> workgroup by the unit's weighted midpoint: nondecreasing, every workgroup ~cw of cost
+    std::vector<int> idx(k.G + 1 + 2 * k.ntile, units);   // [wg_unit (G + 1)][tile_wg (2 ntile)]
+    std::vector<int> vu(units);
+    int64_t pos = 0;
+    int vcur = 0;
+    idx[0] = 0;
+    for (int u = 0; u < units; ++u) {
+      const int w = wt[u / k.S];
+      const int v = (int)std::min<int64_t>(k.G - 1, (2 * pos + w) / (2 * cw));
+      while (vcur < v) idx[++vcur] = u;
+      vu[u] = v;
+      pos += w;
     }
+    for (int t = 0; t < k.ntile; ++t) {
+      idx[k.G + 1 + 2 * t] = vu[t * k.S];
+      idx[k.G + 1 + 2 * t + 1] = vu[t * k.S + k.S - 1];
+    }
+    for (int v = 0; v < k.G; ++v)                 // partial slots: the tiles one workgroup's units touch
+      if (idx[v] < idx[v + 1]) k.J = std::max(k.J, (idx[v + 1] - 1) / k.S - idx[v] / k.S + 1);
     void* d = nullptr;
     TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
     k.tiles = static_cast<const DwTile*>(d);
+    TD3_RC(upload(h, owned, idx.data(), idx.size() * sizeof(int), &d));
+    k.wg_unit = static_cast<const int*>(d);
+    k.tile_wg = k.wg_unit + k.G + 1;
     void* slab = nullptr;
-    TD3_HIP(hipMalloc(&slab, (size_t)k.G * k.J * 4096 * sizeof(float)));
+    TD3_HIP(hipMalloc(&slab, (size_t)k.G * k.J * k.slot * sizeof(float)));
     owned.push_back(slab);
     k.slab = static_cast<float*>(slab);
     st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw_split(a, k, s); }, flops,
-                  std::string("td3::dwsk_kernel<") + (unit_scale ? "true>" : "false>")});
+                  std::string("td3::dwsk_kernel<") + (unit_scale ? "true, " : "false, ") +
+                      (tm == 128 ? "true>" : "false>")});
   } else {
     st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw(a, blocks, s); }, flops,
                   std::string(tile64 ? "td3::dw64_kernel<" : "td3::dw_kernel<") + (unit_scale ? "true>" : "false>")});

@@ -9,6 +9,8 @@
 * ``ReplayBuffer_particles.save / load`` (my_replay_buffer.py:28-44) round trip.
 Tolerances as tests/test_gpu_parity.py.
 """
+import contextlib
+import copy
 import os
 import pickle
 from collections import OrderedDict
@@ -28,6 +30,28 @@ def _states(S, n, seed):
     f = rs.standard_normal((n, S["F"])).astype(np.float32)
     p = rs.standard_normal((n, S["N"], S["D"])).astype(np.float32)
     return f, p
+
+
+@contextlib.contextmanager
+def _oracle_f64():
+    """The oracle's arithmetic in float64 (its dtype is the module's ``f32`` alias): the exact
+    reference value against which the GPU's and the float32 oracle's rounding are both measured."""
+    old = orc.f32, orc.LN_EPS
+    orc.f32, orc.LN_EPS = np.float64, np.float64(1e-5)
+    try:
+        yield
+    finally:
+        orc.f32, orc.LN_EPS = old
+
+
+def _as_f64(L):
+    """A copy of oracle learner ``L`` whose parameters, targets and Adam moments are float64."""
+    L64 = copy.deepcopy(L)
+    for d in (L64.actor, L64.actor_m, L64.actor_v, L64.actor_target,
+              L64.critic, L64.critic_m, L64.critic_v, L64.critic_target):
+        for k in d:
+            d[k] = np.asarray(d[k], dtype=np.float64)
+    return L64
 
 
 def _oracle_after(S, steps, seed):
@@ -51,6 +75,9 @@ def test_actor_learn_matches_oracle(name):
     for k in range(2):
         _load_oracle_state(pol, L)
         f, p = _states(S, 32, 100 + k)
+        L64 = _as_f64(L)
+        with _oracle_f64():
+            orc.particle_actor_learn(L64, f.astype(np.float64), p.astype(np.float64))
         rec = orc.particle_actor_learn(L, f, p)
         loss = pol._actor_learn(torch.from_numpy(f), torch.from_numpy(p), stats=True)
         np.testing.assert_allclose(loss, rec["actor_loss"], rtol=1e-5, atol=1e-7)
@@ -60,13 +87,14 @@ def test_actor_learn_matches_oracle(name):
         for kk, v in pol.critic.numpy_dict().items():          # the critic is only read
             np.testing.assert_array_equal(v, L.critic[kk])
         assert pol._counters() == (L.total_it, L.critic_step, L.actor_step)
-        # exp_avg = 0.9 m + 0.1 g: the actor gradient at the SURVEY §8c gradient tolerance, relative to
-        # each tensor's largest element; the encoder layers (conv1 / conv2: sums over B*N particle rows
-        # of mixed-sign products at the end of the longest backward chain) at 1e-3
+        # exp_avg = 0.9 m + 0.1 g carries the actor gradient, the end of a 7-stage backward chain
+        # (Q1 backward, dQ1/da, tanh, actor MLP, encoder): measured against the float64 oracle, the
+        # GPU's error is at most 3x the float32 oracle's own (or 2e-4 of the tensor's scale)
         sd = pol.actor_optimizer.state_dict()
         for i, kk in enumerate(L.actor):
-            tol = 1e-3 if kk.startswith(("conv1.", "conv2.")) else 2e-4
-            assert _rel_to_max(sd["state"][i]["exp_avg"].numpy(), L.actor_m[kk]) <= tol, kk
+            gpu, ref = sd["state"][i]["exp_avg"].numpy(), L64.actor_m[kk]
+            e_gpu, e_orc = _rel_to_max(gpu, ref), _rel_to_max(L.actor_m[kk], ref)
+            assert e_gpu <= max(3 * e_orc, 2e-4), (kk, e_gpu, e_orc)
 
 
 def test_actor_learn_between_train_steps():
