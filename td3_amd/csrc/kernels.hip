@@ -2569,6 +2569,9 @@ __global__ __launch_bounds__(512, T128 ? 1 : 2) void dwsk_kernel(DwArgs a, DwSpl
   int u = k.wg_unit[v];
   const int u1 = k.wg_unit[v + 1];
   int j = 0;
+#ifdef TD3_TL
+  int nmat = 0, nvec = 0;
+#endif
   while (u < u1) {
     const int t = __builtin_amdgcn_readfirstlane(u / k.S);
     const int s0 = u - t * k.S;
@@ -2585,9 +2588,22 @@ __global__ __launch_bounds__(512, T128 ? 1 : 2) void dwsk_kernel(DwArgs a, DwSpl
       dwsk_vector<SC>(a, P, ta, s0, s1, sm, out);
     }
     u += s1 - s0;
+#ifdef TD3_TL
+    if (T.kind == 0) nmat += s1 - s0;
+    else nvec += s1 - s0;
+    if (j == 0) TL_MARK(1);
+    if (j == 1) TL_MARK(2);
+#endif
     ++j;
   }
   TL_MARK(3);
+#ifdef TD3_TL
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    td3_tl[blockIdx.x][5] = nmat;
+    td3_tl[blockIdx.x][6] = nvec;
+    td3_tl[blockIdx.x][7] = j;
+  }
+#endif
 }
 
 // Four workgroups per tile (a quarter of a matrix tile's rows each; a vector tile uses the first):
