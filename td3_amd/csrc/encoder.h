@@ -32,8 +32,9 @@ struct EncFwdProb {
   float* out; int ldo;     // pooled features -> out[b * ldo + c], c < 128
   uint64_t* mask;          // nullable: ReLU bits for the backward: conv2 [Bp][ntile][64] words
                            // (word j*16+r: channel tile j, MFMA reg r), then conv1
-                           // [Bp][ntile][2][64] words (half g, lane L: channels 32(4g+L/16)+L%16
-                           // low / +16 high, bit R = tile row R), then float counts of the
+                           // [Bp][ntile][2][64] words (half g, lane L = 16(c&3) + r of chunk
+                           // c = 4g + L/16: channel 32c + crow(r) low / + 4 high, crow(r) =
+                           // (r&3) + 8(r>>2), bit R = tile row R), then float counts of the
                            // positive conv2 rows [Bp][128]
 };
 

@@ -1,14 +1,14 @@
 // Particle set encoder (TD3_particles) on gfx950: fused forward and backward.
 //
-//   enc_fwd_kernel   conv1 (1xD) + ReLU computed in registers as the MFMA A operand,
-//                    conv2 (256->128) on v_mfma_f32_32x32x2_f32 with W2 staged once per
+//   enc_fwd_kernel   conv1 (1xD) + ReLU on MFMA (transposed: its output registers are the conv2
+//                    A operand), conv2 (256->128) on v_mfma_f32_32x32x2_f32 with W2 staged once per
 //                    workgroup in LDS, ReLU, the mean over particles and the pool ReLU in the
 //                    epilogue (TD3_particles.py:52-58 / :103-109).  Neither h1 [B*N][256] nor
 //                    h2 [B*N][128] touches HBM: only their ReLU bits (1 bit per element, from
 //                    wave ballots) are kept for the backward.
-//   enc_bwd_kernel   the backward of the same: role A workgroups form dh1 = dz2*W2 and dW1,
-//                    db1 (relu'(z1) from the conv1 bits); role B workgroups dW2 and db2 with h1
-//                    recomputed from the particles.
+//   enc_bwd_kernel   the backward of the same, one pass over each staged particle tile: role A
+//                    forms dh1 = dz2*W2 and dW1, db1 (relu'(z1) from the conv1 bits); role B dW2
+//                    and db2 with h1 recomputed from the particles.
 //   enc_adam_kernel  fixed-order sum of the per-workgroup partial slabs, then torch Adam
 //                    (+ Polyak), or the grad arena on the all-reduced path.
 //
@@ -37,6 +37,10 @@ __device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t val, int la
 __device__ __forceinline__ float lane_select(uint64_t m, float v) {
   return __builtin_amdgcn_inverse_ballot_w64(m) ? v : 0.f;
 }
+
+// mfma_row(r, lane) = crow(r) + 4 * (lane >> 5): the r-dependent part is a compile-time constant
+// after unrolling, so LDS addresses are one lane base + an immediate offset per r.
+__device__ __forceinline__ constexpr int crow(int r) { return (r & 3) + 8 * (r >> 2); }
 
 // ================================================================== forward
 constexpr int kEncS2 = 260;    // LDS row stride of W2 [128][256] (== 4 mod 64: b128 conflict-free)
@@ -80,63 +84,63 @@ __global__ __launch_bounds__(512) void enc_fwd_kernel(EncFwdArgs a) {
   uint64_t* mask1 = P.mask ? P.mask + (size_t)a.Bp * a.ntile * 64 : nullptr;
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
   float npos[4] = {0.f, 0.f, 0.f, 0.f};                // rows with conv2 output > 0 (backward db2)
+  // conv1 on MFMA, transposed: per 32-channel chunk c, z1^T[channel][particle] = W1 x^T + b1 on
+  // v_mfma_f32_32x32x2_f32 (A = W1[32c + i][2s + h], B = x[particle i][2s + h]; K = D rounded up
+  // to even, k in order: the fmaf chain b1 + sum_d W1[k][d] x[d] of role B's recompute, bitwise).
+  // Lane (i, h) then holds h1[particle i][channel 32c + crow(r) + 4h] in register r, which IS the
+  // conv2 A operand when conv2's reduction runs over the chunk's channels in the order
+  // k(s, h) = crow(s) + 4h: its B operand W2[j*32 + i][32c + 4h + 8q + e] (s = 4q + e) is four
+  // float4 LDS reads.  No VALU conv1, no register shuffle.
+  constexpr int KS = (DK + 1) / 2;                        // conv1 MFMA steps (features 2s, 2s + 1)
   for (int t = 0; t < a.ntile; ++t) {
     const int n = t * 32 + i;
-    float x[DK];
+    float xk[KS];
 #pragma unroll
-    for (int d = 0; d < DK; ++d) x[d] = part_ld(base, n, a.N, D, d);
+    for (int s = 0; s < KS; ++s) xk[s] = part_ld(base, n, a.N, D, 2 * s + h);
     f32x16 acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
     uint32_t m1lo = 0, m1hi = 0;
-#pragma unroll 1
-    for (int c = 0; c < kEncC1 / 32; ++c) {
-      // A operand: h1[n][k] = relu(b1[k] + sum_d W1[k][d] x[n][d]), k = 32c + 16h + s
-      const int k0 = c * 32 + 16 * h;
-      float av[16];
+    auto conv1 = [&](int c, f32x16& z) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(b1s + k0 + 4 * q);
-        av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
+        const float4 v = *reinterpret_cast<const float4*>(b1s + c * 32 + 4 * h + 8 * q);
+        z[4 * q + 0] = v.x; z[4 * q + 1] = v.y; z[4 * q + 2] = v.z; z[4 * q + 3] = v.w;
       }
 #pragma unroll
-      for (int d = 0; d < DK; ++d) {
-        float xd = x[d];
-        asm volatile("" : "+v"(xd));         // no loop-invariant splats of x hoisted out of c
+      for (int s = 0; s < KS; ++s) z = mfma32x32x2(w1t[(2 * s + h) * kEncC1 + c * 32 + i], xk[s], z);
+    };
+    f32x16 zn;
+    conv1(0, zn);
+#pragma unroll 1
+    for (int c = 0; c < kEncC1 / 32; ++c) {
+      float av[16];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 w = *reinterpret_cast<const float4*>(w1t + d * kEncC1 + k0 + 4 * q);
-          av[4 * q + 0] = __fmaf_rn(w.x, xd, av[4 * q + 0]);
-          av[4 * q + 1] = __fmaf_rn(w.y, xd, av[4 * q + 1]);
-          av[4 * q + 2] = __fmaf_rn(w.z, xd, av[4 * q + 2]);
-          av[4 * q + 3] = __fmaf_rn(w.w, xd, av[4 * q + 3]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 16; ++s) av[s] = fmaxf(av[s], 0.f);
+      for (int r = 0; r < 16; ++r) av[r] = fmaxf(zn[r], 0.f);
+      if (c + 1 < kEncC1 / 32) conv1(c + 1, zn);          // next chunk's conv1 in the shadow of this one's conv2
       if (mask1) {
-        // conv1 ReLU bits: ballot s of chunk c = rows of channels 32c+s (low) / 32c+16+s (high);
-        // lane (c&3)*16+s keeps it, and every 4 chunks the wave stores 64 words
+        // conv1 ReLU bits: ballot r of chunk c = the 32 particles of channel 32c + crow(r) (low) /
+        // 32c + crow(r) + 4 (high); lane (c&3)*16+r keeps it, every 4 chunks the wave stores 64 words
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const uint64_t w = __ballot(av[s] > 0.f);
-          m1lo = writelane(m1lo, (uint32_t)w, (c & 3) * 16 + s);
-          m1hi = writelane(m1hi, (uint32_t)(w >> 32), (c & 3) * 16 + s);
+        for (int r = 0; r < 16; ++r) {
+          const uint64_t w = __ballot(av[r] > 0.f);
+          m1lo = writelane(m1lo, (uint32_t)w, (c & 3) * 16 + r);
+          m1hi = writelane(m1hi, (uint32_t)(w >> 32), (c & 3) * 16 + r);
         }
         if ((c & 3) == 3)
           *(GAS uint64_t*)(mask1 + (((size_t)b * a.ntile + t) * 2 + (c >> 2)) * 64 + lane) =
               ((uint64_t)m1hi << 32) | m1lo;
       }
-      // B operand: W2[j*32 + i][k]; conv2 output tile j (32 channels)
+      // B operand: W2[j*32 + i][32c + 4h + crow(s)]; conv2 output tile j (32 channels)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float* wr = w2s + (j * 32 + i) * kEncS2 + k0;
+        const float* wr = w2s + (j * 32 + i) * kEncS2 + c * 32 + 4 * h;
         float bv[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(wr + 4 * q);
+          const float4 v = *reinterpret_cast<const float4*>(wr + 8 * q);
           bv[4 * q + 0] = v.x; bv[4 * q + 1] = v.y; bv[4 * q + 2] = v.z; bv[4 * q + 3] = v.w;
         }
 #pragma unroll
@@ -186,20 +190,17 @@ constexpr int kEncBufs = 2;      // staging double buffer: tile it+1 lands while
 // role A stages W2^T [256][132]; role B keeps h1 in registers
 
 template <int ROLE>
-constexpr int enc_big() { return ROLE == 0 ? kEncC1 * kEncST : 0; }
+constexpr int enc_big() { return ROLE != 1 ? kEncC1 * kEncST : 0; }
 template <int ROLE>
 constexpr int enc_bwd_lds() {
   return (enc_big<ROLE>() + kEncC1 * kEncS1 + kEncBufs * (32 * kEncMaxD + 64 * 2 + kEncC2) + kEncC1) * 4;
 }
-static_assert(enc_bwd_lds<0>() <= 160 * 1024, "encoder backward LDS");
+static_assert(enc_bwd_lds<2>() <= 160 * 1024, "encoder backward LDS");
 
 // rows of the forward's ballot words: word (j, r) holds channel j*32 + lane&31 of row
 // mfma_row(r, lane); row R lives in word r = (R&3) + 4(R>>3), half (R>>2)&1.
 __device__ __forceinline__ int word_of_row(int R) { return (R & 3) + 4 * (R >> 3); }
 __device__ __forceinline__ int half_of_row(int R) { return (R >> 2) & 1; }
-// mfma_row(r, lane) = crow(r) + 4 * (lane >> 5): the r-dependent part is a compile-time constant
-// after unrolling, so LDS addresses are one lane base + an immediate offset per r.
-__device__ __forceinline__ constexpr int crow(int r) { return (r & 3) + 8 * (r >> 2); }
 
 // Pooled-feature grad of every batch row (one wave per row): LN_in backward of the MLP input
 // grad (no ReLU before lnorm1), then the pool ReLU (pooled > 0) and the 1/N of the mean.
@@ -230,8 +231,11 @@ __global__ __launch_bounds__(256) void enc_gpool_kernel(EncBwdArgs a) {
   }
 }
 
+// ROLE 0: role A only, 1: role B only, 2: both on every staged tile (one pass over the particles,
+// masks and pooled grads; the role B h1 recompute and dW2 MFMAs interleave with role A's chains)
 template <int DK, int ROLE>
 __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
+  constexpr bool kA = ROLE != 1, kB = ROLE != 0;
   extern __shared__ float4 sm4[];
   float* big = reinterpret_cast<float*>(sm4);           // role A: W2^T [256][132]
   float* w1s = big + enc_big<ROLE>();                   // [256][17]
@@ -244,13 +248,13 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   const int wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
   const float* W1 = P.enc + EncOff::w1(D);
   const float* W2 = P.enc + EncOff::w2(D);
-  if constexpr (ROLE == 0) {
+  if constexpr (kA) {
     for (int e = tid; e < kEncC2 * kEncC1; e += 512) {     // W2^T: row k, column c
       const int c = e >> 8, k = e & 255;
       big[k * kEncST + c] = gld(W2 + e);
     }
   }
-  if constexpr (ROLE == 1) {
+  if constexpr (kB) {
     for (int e = tid; e < kEncC1 * kEncMaxD; e += 512) {
       const int k = e >> 4, d = e & 15;
       if (d < D) w1s[k * kEncS1 + d] = gld(W1 + k * D + d);
@@ -261,20 +265,20 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   __syncthreads();
 
   const int k_own = wave * 32 + i;                      // this lane's conv1 channel (h1 tiles)
-  float w1r[ROLE == 1 ? DK : 1];
+  float w1r[kB ? DK : 1];
   float b1k = 0.f;
-  if constexpr (ROLE == 1) {
+  if constexpr (kB) {
 #pragma unroll
     for (int d = 0; d < DK; ++d) w1r[d] = w1s[k_own * kEncS1 + d];
     b1k = b1s[k_own];
   }
 
   f32x16 accW1;                                         // role A: dW1 tile
-  f32x16 accB[ROLE == 1 ? 4 : 1];                       // role B: dW2 tiles
+  f32x16 accB[kB ? 4 : 1];                              // role B: dW2 tiles
 #pragma unroll
   for (int r = 0; r < 16; ++r) accW1[r] = 0.f;
 #pragma unroll
-  for (int q = 0; q < (ROLE == 1 ? 4 : 1); ++q)
+  for (int q = 0; q < (kB ? 4 : 1); ++q)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accB[q][r] = 0.f;
   float gb1 = 0.f;
@@ -289,16 +293,18 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   float st_x = 0.f, st_g = 0.f;
   uint64_t st_m = 0;
   // role A: the forward's conv1 ReLU word of channel k_own (bit R = row R of the tile)
-  const uint64_t* mask1 = P.mask + (size_t)a.Bp * a.ntile * 64 + (wave >> 2) * 64 + (wave & 3) * 16 + (i & 15);
-  const int m1_sh = 32 * (i >> 4);
+  // (channel 32c + m sits in the forward's ballot r = (m & 3) + 4 (m >> 3) of chunk c, half (m >> 2) & 1)
+  const uint64_t* mask1 = P.mask + (size_t)a.Bp * a.ntile * 64 + (wave >> 2) * 64 + (wave & 3) * 16 +
+                          ((i & 3) + 4 * (i >> 3));
+  const int m1_sh = 32 * ((i >> 2) & 1);
   uint32_t st_r = 0;
   auto fetch = [&](int it) {
     const int b = b_begin + it / a.ntile, t = it % a.ntile;
     const float* base = a.data + (size_t)a.idx[b] * a.rec + P.part_off;
     st_x = part_ld(base, t * 32 + srow, a.N, D, sd);
-    if (ROLE == 0 && tid < 64) st_m = *(const GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + tid);
+    if (kA && tid < 64) st_m = *(const GAS uint64_t*)(P.mask + ((size_t)b * a.ntile + t) * 64 + tid);
     if (tid < kEncC2) st_g = gld(P.gpool + ((size_t)b * kEncC2 + tid));
-    if constexpr (ROLE == 0) st_r = (uint32_t)(*(const GAS uint64_t*)(mask1 + ((size_t)b * a.ntile + t) * 128) >> m1_sh);
+    if constexpr (kA) st_r = (uint32_t)(*(const GAS uint64_t*)(mask1 + ((size_t)b * a.ntile + t) * 128) >> m1_sh);
   };
   // ---- dh1 tile (rows i, channels k_own): A = dz2[row i][c], B = W2^T[k][c]
   auto role_a_dh1 = [&](f32x16& ac, const uint64_t* mb, const float* gsb) {
@@ -345,17 +351,18 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
     uint64_t* mb = ms + buf * 64;
     float* gsb = gs + buf * kEncC2;
     xb[srow * kEncMaxD + sd] = st_x;
-    if (ROLE == 0 && tid < 64) mb[tid] = st_m;
+    if (kA && tid < 64) mb[tid] = st_m;
     if (tid < kEncC2) gsb[tid] = st_g;
     const uint32_t rb_now = st_r;
     __syncthreads();
     if (it + 1 < ntot) fetch(it + 1);
     {
-      if constexpr (ROLE == 0) {
+      if constexpr (kA) {
         f32x16 acc;
         role_a_dh1(acc, mb, gsb);
         role_a_dw1(acc, xb, rb_now);
-      } else {
+      }
+      if constexpr (kB) {
         // ---- h1 of this wave's channels k_own at rows crow(r) + 4h, kept in registers as the
         // B operand: lane (i, h) of step s supplies h1[row crow(s)+4h][k_own].
         // A = dz2[row crow(s)+4h][mt*32 + i]: the forward's ballot word (mt, s) has bit
@@ -406,7 +413,7 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   }
   // ---- partial slab of this workgroup
   float* out = P.partial + (size_t)g * EncOff::size(D);
-  if constexpr (ROLE == 0) {
+  if constexpr (kA) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k = wave * 32 + mfma_row(r, lane);
@@ -414,7 +421,8 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
     }
     const float v = gb1 + __shfl_xor(gb1, 32, 64);
     if (h == 0) gst(out + (EncOff::b1(D) + k_own), v);
-  } else {
+  }
+  if constexpr (kB) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -458,6 +466,9 @@ __global__ __launch_bounds__(256) void enc_adam_kernel(EncAdamArgs a) {
 }
 
 // ================================================================== launchers
+#ifndef TD3_ENC_FUSED
+#define TD3_ENC_FUSED 1      // one launch running roles A and B on each staged tile (0: two launches)
+#endif
 int launch_enc_fwd(const EncFwdArgs& a, hipStream_t s) {
   if (a.Bp <= 0 || a.nprob <= 0) return 0;
   if (a.D > kEncMaxD || a.nprob > kMaxEnc) {
@@ -483,9 +494,13 @@ int launch_enc_bwd(const EncBwdArgs& a, hipStream_t s) {
   }
   hipLaunchKernelGGL(enc_gpool_kernel, dim3((a.B + 3) / 4, a.nprob), dim3(256), 0, s, a);
   const dim3 grid(a.nwg, a.nprob);
+#if TD3_ENC_FUSED
+#define TD3_ENC_BWD(DK) hipLaunchKernelGGL((enc_bwd_kernel<DK, 2>), grid, dim3(512), enc_bwd_lds<2>(), s, a)
+#else
 #define TD3_ENC_BWD(DK)                                                                        \
   hipLaunchKernelGGL((enc_bwd_kernel<DK, 0>), grid, dim3(512), enc_bwd_lds<0>(), s, a);       \
   hipLaunchKernelGGL((enc_bwd_kernel<DK, 1>), grid, dim3(512), enc_bwd_lds<1>(), s, a)
+#endif
   switch ((a.D + 3) / 4) {
     case 1: TD3_ENC_BWD(4); break;
     case 2: TD3_ENC_BWD(8); break;
@@ -512,6 +527,8 @@ static int enc_attr() {
                               enc_bwd_lds<0>()));
   TD3_HIP(hipFuncSetAttribute((const void*)enc_bwd_kernel<DK, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               enc_bwd_lds<1>()));
+  TD3_HIP(hipFuncSetAttribute((const void*)enc_bwd_kernel<DK, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              enc_bwd_lds<2>()));
   return 0;
 }
 
