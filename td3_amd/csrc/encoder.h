@@ -80,6 +80,9 @@ struct EncAdamProb {
   int64_t off;                      // encoder block offset inside the group arenas
 };
 
+#ifndef TD3_ENC_FUSED
+#define TD3_ENC_FUSED 1      // enc_bwd_kernel<DK, 2>: roles A and B on each staged tile (0: two launches)
+#endif
 int launch_enc_fwd(const EncFwdArgs& a, hipStream_t s);
 int launch_enc_bwd(const EncBwdArgs& a, hipStream_t s);
 // sum of the partial slabs -> grad -> Adam (+ Polyak) or the grad arena (mode = DwMode)

@@ -110,7 +110,8 @@ __global__ __launch_bounds__(512) void enc_fwd_kernel(EncFwdArgs a) {
         z[4 * q + 0] = v.x; z[4 * q + 1] = v.y; z[4 * q + 2] = v.z; z[4 * q + 3] = v.w;
       }
 #pragma unroll
-      for (int s = 0; s < KS; ++s) z = mfma32x32x2(w1t[(2 * s + h) * kEncC1 + c * 32 + i], xk[s], z);
+      for (int s = 0; s < KS; ++s)
+        if (2 * s < D) z = mfma32x32x2(w1t[(2 * s + h) * kEncC1 + c * 32 + i], xk[s], z);   // ceil(D/2) steps
     };
     f32x16 zn;
     conv1(0, zn);
@@ -273,10 +274,13 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
     b1k = b1s[k_own];
   }
 
-  f32x16 accW1;                                         // role A: dW1 tile
+  // role A: dW1[k_own][d] of this lane's rows (crow(s) + 4h), on the VALU: as a 32x32x2 MFMA
+  // tile its N would be the D (<= 16) particle features, 72 % of the MFMA issue wasted at D = 9;
+  // the lane's 16 x DK FMAs run beside the other wave's MFMA chain instead
+  float w1acc[kA ? DK : 1];
   f32x16 accB[kB ? 4 : 1];                              // role B: dW2 tiles
 #pragma unroll
-  for (int r = 0; r < 16; ++r) accW1[r] = 0.f;
+  for (int d = 0; d < (kA ? DK : 1); ++d) w1acc[d] = 0.f;
 #pragma unroll
   for (int q = 0; q < (kB ? 4 : 1); ++q)
 #pragma unroll
@@ -334,16 +338,23 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   // ---- dz1 = relu'(z1) dh1 at (row mfma_row(r), channel k_own), relu'(z1) from the forward's
   // conv1 bits (rb: bit R = tile row R); db1; dW1 += dz1^T x
   auto role_a_dw1 = [&](const f32x16& ac, const float* xb, uint32_t rb) {
-    const float* xcol = xb + 4 * h * kEncMaxD + (i & 15);
     rb >>= 4 * h;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const float gz = ((rb >> crow(s)) & 1u) ? ac[s] : 0.f;
       gb1 += gz;
-      const float xv = i < kEncMaxD ? xcol[crow(s) * kEncMaxD] : 0.f;
-      accW1 = mfma32x32x2(gz, xv, accW1);
+      const float* xr = xb + (crow(s) + 4 * h) * kEncMaxD;   // one row per lane half: broadcast reads
+#pragma unroll
+      for (int q = 0; q < DK / 4; ++q) {
+        const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * q);
+        w1acc[4 * q + 0] = __fmaf_rn(gz, xv.x, w1acc[4 * q + 0]);
+        w1acc[4 * q + 1] = __fmaf_rn(gz, xv.y, w1acc[4 * q + 1]);
+        w1acc[4 * q + 2] = __fmaf_rn(gz, xv.z, w1acc[4 * q + 2]);
+        w1acc[4 * q + 3] = __fmaf_rn(gz, xv.w, w1acc[4 * q + 3]);
+      }
     }
   };
+
   if (ntot > 0) fetch(0);
   for (int it = 0; it < ntot; ++it) {
     const int buf = it % kEncBufs;
@@ -367,7 +378,8 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
         // B operand: lane (i, h) of step s supplies h1[row crow(s)+4h][k_own].
         // A = dz2[row crow(s)+4h][mt*32 + i]: the forward's ballot word (mt, s) has bit
         // i + 32h = lane for exactly that element, so one v_cndmask on the word (scalar
-        // loaded, one channel tile ahead) builds each operand
+        // loaded, one channel tile ahead) builds each operand (read from the staged tile in LDS
+        // and made uniform by v_readfirstlane instead: CB_enc 3.99 -> 4.15 ms)
         const uint64_t* mw = P.mask + ((size_t)(b_begin + it / a.ntile) * a.ntile + it % a.ntile) * 64;
         uint64_t wq[16];
 #pragma unroll
@@ -415,9 +427,9 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   float* out = P.partial + (size_t)g * EncOff::size(D);
   if constexpr (kA) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k = wave * 32 + mfma_row(r, lane);
-      if (i < D) gst(out + (EncOff::w1(D) + (int64_t)k * D + i), accW1[r]);
+    for (int d = 0; d < DK; ++d) {                         // lane halves: rows +0 / +4 of each group
+      const float v = w1acc[d] + __shfl_xor(w1acc[d], 32, 64);
+      if (h == 0 && d < D) gst(out + (EncOff::w1(D) + (int64_t)k_own * D + d), v);
     }
     const float v = gb1 + __shfl_xor(gb1, 32, 64);
     if (h == 0) gst(out + (EncOff::b1(D) + k_own), v);
@@ -466,9 +478,6 @@ __global__ __launch_bounds__(256) void enc_adam_kernel(EncAdamArgs a) {
 }
 
 // ================================================================== launchers
-#ifndef TD3_ENC_FUSED
-#define TD3_ENC_FUSED 1      // one launch running roles A and B on each staged tile (0: two launches)
-#endif
 int launch_enc_fwd(const EncFwdArgs& a, hipStream_t s) {
   if (a.Bp <= 0 || a.nprob <= 0) return 0;
   if (a.D > kEncMaxD || a.nprob > kMaxEnc) {

@@ -1421,7 +1421,7 @@ static void push_enc_bwd(td3_handle* h, Plan* P, std::vector<Stage>& st, const s
                   a.nwg = enc_bwd_nwg(P->B, (int)items.size());
                   return launch_enc_bwd(a, s);
                 },
-                flops, "td3::enc_bwd_kernel<" + std::to_string(((D + 3) / 4) * 4) + ", 0>"});
+                flops, "td3::enc_bwd_kernel<" + std::to_string(((D + 3) / 4) * 4) + (TD3_ENC_FUSED ? ", 2>" : ", 0>")});
 }
 
 static void destroy_graphs(Plan* P) {
