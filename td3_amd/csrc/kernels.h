@@ -63,8 +63,15 @@ enum RowKind : int {
 #ifndef TD3_GEMM_NW16
 #define TD3_GEMM_NW16 1
 #endif
+// WN = kWn4x2 (B >= 512): the WN = 4 workgroup over TWO 32-row tiles, 64 x 128 outputs, each
+// wave's 32 weight columns reused for both (half the weight stream per MAC of WN = 4); prologue
+// kinds Copy / LN / LN-bwd / head-bwd only; 8 waves, one workgroup per CU (A rows 2 x 32 x Kp).
+constexpr int kWn4x2 = 12;
+constexpr int wn_cols(int wn) { return wn == kWn4x2 ? 4 : wn; }   // 32-column waves of a K group
+constexpr int wn_rt(int wn) { return wn == kWn4x2 ? 2 : 1; }      // 32-row tiles per workgroup
 constexpr int gemm_nw(int mode, int wn, int pro) {
-  return (TD3_GEMM_NW16 && pro != kProL0 && pro != kProL0G && (mode == 1 || wn == 0)) ? 16 : kGemmWaves;
+  return (TD3_GEMM_NW16 && wn != kWn4x2 && pro != kProL0 && pro != kProL0G && (mode == 1 || wn == 0)) ? 16
+                                                                                                   : kGemmWaves;
 }
 
 constexpr int kMaxEx = 24;

@@ -1183,15 +1183,17 @@ __device__ __forceinline__ int xcd_tile(int nb) {
 template <int MODE, int WN, int PRO, int NW = kNW>
 __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, int tb3, int Bp, const GemmTable& tab,
                                           Counters* bump, int bump_actor, float* smem) {
-  constexpr int RPW = 32 / NW;                 // prologue rows per wave
+  constexpr int RT = wn_rt(WN);                // 32-row tiles of the workgroup (kWn4x2: 2)
+  constexpr int RPW = 32 * RT / NW;            // prologue rows per wave
   static_assert(NW == kNW || (PRO != kProL0 && PRO != kProL0G), "fused layer 0 runs kNW waves");
+  static_assert(RT == 1 || (PRO != kProL0 && PRO != kProL0G && PRO != kProGather), "two row tiles: plain prologues");
   // WN = 0: 16 output columns per workgroup on v_mfma_f32_16x16x4_f32 (two 16-row halves of the
   // 32-row tile): half the MFMA chain of WN = 1 for stages of <= 128 32-column workgroups, which
   // otherwise leave half the CUs idle (td3.hip gemm_wn)
-  constexpr int WNS = WN == 0 ? 1 : WN;        // waves per K group
+  constexpr int WNS = WN == 0 ? 1 : wn_cols(WN);   // waves per K group
   constexpr int WK = NW / WNS;
   constexpr int NT = 64 * NW;                  // threads
-  constexpr int OUTW = WN == 0 ? 16 : 32 * WN; // output columns of the workgroup
+  constexpr int OUTW = WN == 0 ? 16 : 32 * wn_cols(WN);   // output columns of the workgroup
   constexpr bool kPrefetchB = true;
   int pi = 0;
   if (nprob > 1 && b >= tb1) pi = 1;
@@ -1230,13 +1232,13 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
                    "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
                    "s"(tab.rs.ctr));
   }
-  const int mtiles = Bp >> 5;
+  const int mtiles = (Bp >> 5) / RT;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
 #if defined(TD3_TL) && !defined(TD3_TL_FINE)
   if (threadIdx.x == 0 && blockIdx.x < 8192) td3_tl[blockIdx.x][4] |= (unsigned long long)(nt + 1) << 16;
 #endif
-  const int m0 = mt << 5;
+  const int m0 = mt * 32 * RT;
   const int n0 = nt * OUTW;
   const int Kp = P.Kp;
   const int S = lds_stride(Kp);
@@ -1336,7 +1338,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
   __syncthreads();
   TL_MARK(1);
   if constexpr (PRO != kProLN && !kL0) issue_stream();
-  if constexpr (WN == 4) {
+  if constexpr (wn_cols(WN) == 4) {
     if (s0 < ce) load_chunk<MODE>(P, bs0, s0, ncol, h);
     if (s0 + 1 < ce) load_chunk<MODE>(P, bs1, s0 + 1, ncol, h);
   }
@@ -1371,45 +1373,39 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
       }
     }
   }
-  f32x16 acc;
+  f32x16 acc[RT];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
+  // one 32-deep K chunk: per row tile, the lane's 16 A values (4 ds_read_b128) and 16 MFMAs on the
+  // chunk's weight fragment (the row tiles' chains are independent: interleaved)
+  auto chunk = [&](const float* arow, int kb, const float (&b)[16]) {
+    float av[RT][16];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(arow + rt * 32 * S + kb + 4 * q);
+        av[rt][4 * q + 0] = v.x; av[rt][4 * q + 1] = v.y; av[rt][4 * q + 2] = v.z; av[rt][4 * q + 3] = v.w;
+      }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32x32x2(av[rt][s], b[s], acc[rt]);
+  };
   if (WN != 0 && active) {
     const float* arow = smem + i * S + 16 * h;
 #pragma unroll
-    for (int cc = 0; cc < kCh; ++cc) {
-      if (cb + cc < ce) {
-        const int kb = (cb + cc) * 32;
-        float av[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(arow + kb + 4 * q);
-          av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
-        }
-#pragma unroll
-        for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bv[cc][s], acc);
-      }
-    }
+    for (int cc = 0; cc < kCh; ++cc)
+      if (cb + cc < ce) chunk(arow, (cb + cc) * 32, bv[cc]);
     // the streamed chunks: two buffers, chunk ch+2 requested as chunk ch is multiplied
-    if constexpr (WN >= 2) {
+    if constexpr (wn_cols(WN) >= 2) {
       for (int ch = s0; ch < ce; ch += 2) {
-        float av[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(arow + ch * 32 + 4 * q);
-          av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
-        }
-#pragma unroll
-        for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bs0[s], acc);
+        chunk(arow, ch * 32, bs0);
         if (ch + 2 < ce) load_chunk<MODE>(P, bs0, ch + 2, ncol, h);
         if (ch + 1 < ce) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 v = *reinterpret_cast<const float4*>(arow + (ch + 1) * 32 + 4 * q);
-            av[4 * q + 0] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
-          }
-#pragma unroll
-          for (int s = 0; s < 16; ++s) acc = mfma32x32x2(av[s], bs1[s], acc);
+          chunk(arow, (ch + 1) * 32, bs1);
           if (ch + 3 < ce) load_chunk<MODE>(P, bs1, ch + 3, ncol, h);
         }
       }
@@ -1421,44 +1417,49 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
     if (active) {
       const int col = ncol0 + i;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = mfma_row(r, lane);
-        float v = acc[r];
-        if (MODE == 0 && P.bias) v = v + bias;
-        if (P.relu) v = fmaxf(v, 0.f);
-        gst(P.C + ((size_t)(m0 + row) * P.ldc + col), v);
-      }
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rt * 32 + mfma_row(r, lane);
+          float v = acc[rt][r];
+          if (MODE == 0 && P.bias) v = v + bias;
+          if (P.relu) v = fmaxf(v, 0.f);
+          gst(P.C + ((size_t)(m0 + row) * P.ldc + col), v);
+        }
     }
     TL_MARK(2);
   } else {
-    __syncthreads();
-    float* red = smem;  // [NW][32][33]; wave = wk * WNS + wn
-    if constexpr (WN == 0) {
-      // 16x16 C/D map: column lane & 15, row 4 * (lane >> 4) + j
+    float* red = smem;  // [NW][32][33]; wave = wk * WNS + wn; one row tile at a time
 #pragma unroll
-      for (int half = 0; half < 2; ++half)
+    for (int rt = 0; rt < RT; ++rt) {
+      __syncthreads();
+      if constexpr (WN == 0) {
+        // 16x16 C/D map: column lane & 15, row 4 * (lane >> 4) + j
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          red[(wave * 32 + 16 * half + 4 * (lane >> 4) + j) * 33 + (lane & 15)] = acc16[half][j];
-    } else {
+        for (int half = 0; half < 2; ++half)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[r];
-    }
-    __syncthreads();
-    TL_MARK(2);
-    // (32 x OUTW outputs over NT threads: 16 waves of a 16-column tile leave half the threads idle)
+          for (int j = 0; j < 4; ++j)
+            red[(wave * 32 + 16 * half + 4 * (lane >> 4) + j) * 33 + (lane & 15)] = acc16[half][j];
+      } else {
 #pragma unroll
-    for (int q = 0; q < (32 * OUTW + NT - 1) / NT; ++q) {
-      const int e = threadIdx.x + NT * q;
-      if (32 * OUTW % NT != 0 && e >= 32 * OUTW) break;
-      const int row = e / OUTW, colw = e % OUTW;
-      const int wnn = colw >> 5, ci = colw & 31;
-      float v = red[(wnn * 32 + row) * 33 + ci];
+        for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[rt][r];
+      }
+      __syncthreads();
+      TL_MARK(2);
+      // (32 x OUTW outputs over NT threads: 16 waves of a 16-column tile leave half the threads idle)
 #pragma unroll
-      for (int w = 1; w < WK; ++w) v = v + red[((w * WNS + wnn) * 32 + row) * 33 + ci];
-      if (MODE == 0 && P.bias) v = v + bias;
-      if (P.relu) v = fmaxf(v, 0.f);
-      if (n0 + colw < P.Nout) gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + colw), v);
+      for (int q = 0; q < (32 * OUTW + NT - 1) / NT; ++q) {
+        const int e = threadIdx.x + NT * q;
+        if (32 * OUTW % NT != 0 && e >= 32 * OUTW) break;
+        const int row = e / OUTW, colw = e % OUTW;
+        const int wnn = colw >> 5, ci = colw & 31;
+        float v = red[(wnn * 32 + row) * 33 + ci];
+#pragma unroll
+        for (int w = 1; w < WK; ++w) v = v + red[((w * WNS + wnn) * 32 + row) * 33 + ci];
+        if (MODE == 0 && P.bias) v = v + bias;
+        if (P.relu) v = fmaxf(v, 0.f);
+        if (n0 + colw < P.Nout) gst(P.C + ((size_t)(m0 + rt * 32 + row) * P.ldc + n0 + colw), v);
+      }
     }
   }
   TL_MARK(3);
@@ -1480,7 +1481,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
 }
 
 template <int MODE, int WN, int PRO>
-__global__ __launch_bounds__(64 * gemm_nw(MODE, WN, PRO), WN == 4 ? 4 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
+__global__ __launch_bounds__(64 * gemm_nw(MODE, WN, PRO), WN == 4 ? 4 : WN == kWn4x2 ? 2 : 1) void gemm_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
                                                         GemmTable tab, Counters* bump, int bump_actor) {
   extern __shared__ float4 smem4[];
   const int b = xcd_tile(nb);
@@ -1501,7 +1502,7 @@ __global__ __launch_bounds__(64 * gemm_nw(MODE, WN, PRO), WN == 4 ? 4 : 1) void 
 #define TD3_DUAL_OCC 4
 #endif
 template <int M1, int W1, int P1, int M2, int W2, int P2>
-__global__ __launch_bounds__(64 * kNW, (W1 == 4 || W2 == 4) ? 4 : TD3_DUAL_OCC) void gemm2_kernel(
+__global__ __launch_bounds__(64 * kNW, (W1 == 4 || W2 == 4) ? 4 : (W1 == kWn4x2 || W2 == kWn4x2) ? 2 : TD3_DUAL_OCC) void gemm2_kernel(
     int nb1, int nb2, int Bp, int np1, int a1, int a2, int a3, int np2, int c1, int c2, int c3, GemmTable t1,
     GemmTable t2) {
   extern __shared__ float4 smem4[];
@@ -2841,7 +2842,17 @@ static GemmFn pick_bwd(int pro) {
   return nullptr;
 }
 
+static GemmFn pick_4x2(int mode, int pro) {      // kWn4x2: the plain prologues only
+  if (mode == 0 && pro == kProCopy) return gl<0, kWn4x2, kProCopy>;
+  if (mode == 0 && pro == kProLN) return gl<0, kWn4x2, kProLN>;
+  if (mode == 1 && pro == kProCopy) return gl<1, kWn4x2, kProCopy>;
+  if (mode == 1 && pro == kProLNBwd) return gl<1, kWn4x2, kProLNBwd>;
+  if (mode == 1 && pro == kProHeadBwd) return gl<1, kWn4x2, kProHeadBwd>;
+  return nullptr;
+}
+
 static GemmFn pick_gemm(int mode, int wn, int pro) {
+  if (wn == kWn4x2) return pick_4x2(mode, pro);
   if (mode == 0 && wn == 0) return pick_fwd<0>(pro);
   if (mode == 1 && wn == 0) return pick_bwd<0>(pro);
   if (mode == 0 && wn == 1) return pick_fwd<1>(pro);
@@ -2861,7 +2872,8 @@ static GemmFn pick_gemm(int mode, int wn, int pro) {
   X(0, 4, kProL0, 1, 4, kProCopy) X(0, 1, kProLN, 1, 4, kProLNBwd)     \
   X(0, 4, kProCopy, 1, 4, kProCopy) X(0, 4, kProLN, 1, 4, kProLNBwd)   \
   X(0, 0, kProCopy, 1, 0, kProCopy) X(0, 1, kProL0, 1, 0, kProCopy)    \
-  X(0, 0, kProL0, 1, 1, kProCopy) X(0, 1, kProLN, 1, 1, kProLNBwd)
+  X(0, 0, kProL0, 1, 1, kProCopy) X(0, 1, kProLN, 1, 1, kProLNBwd)     \
+  X(0, kWn4x2, kProCopy, 1, kWn4x2, kProCopy) X(0, kWn4x2, kProLN, 1, kWn4x2, kProLNBwd)
 
 int gemm2_supported(int m1, int w1, int p1, int m2, int w2, int p2) {
 #define TD3_G2_Q(A, B, C, D, E, F) \
@@ -3134,7 +3146,12 @@ int kernels_init() {
   if (!rc) rc = set_attr_all<1>();
   if (!rc) rc = set_attr_all<2>();
   if (!rc) rc = set_attr_all<4>();
-  return rc;
+  if (rc) return rc;
+  for (const void* f : {(const void*)gemm_kernel<0, kWn4x2, kProCopy>, (const void*)gemm_kernel<0, kWn4x2, kProLN>,
+                        (const void*)gemm_kernel<1, kWn4x2, kProCopy>, (const void*)gemm_kernel<1, kWn4x2, kProLNBwd>,
+                        (const void*)gemm_kernel<1, kWn4x2, kProHeadBwd>})
+    TD3_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  return 0;
 }
 
 }  // namespace td3

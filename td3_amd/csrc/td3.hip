@@ -375,8 +375,8 @@ static void alloc_eval(Scratch& S, const NetL& n, int Bp, float* X, int ldx, boo
   }
 }
 
-static int gemm_lds_bytes(int Kp) {
-  int f = std::max(32 * lds_stride(Kp), kGemmWaves * 32 * 33);
+static int gemm_lds_bytes(int Kp, int rt = 1) {
+  int f = std::max(32 * rt * lds_stride(Kp), kGemmWaves * 32 * 33);
   return f * 4;
 }
 
@@ -513,7 +513,22 @@ static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd) {
   if (wn1_blocks <= TD3_WN0_MAX) return 0;
   return (fwd && wn1_blocks >= TD3_WN2_MIN) ? 2 : 1;
 }
-static int gemm_outw(int wn) { return wn == 0 ? 16 : 32 * wn; }   // output columns per workgroup
+static int gemm_outw(int wn) { return wn == 0 ? 16 : 32 * wn_cols(wn); }   // output columns per workgroup
+// Two 32-row tiles per 128-column workgroup (kWn4x2, one workgroup per CU) against WN = 4 (two
+// workgroups per CU): a win only for stages of >= 384 WN = 4 workgroups at B <= 2048 (Humanoid
+// F_fwd0 23.9 -> 21.2 us, F_fwd1 30.0 -> 28.8); every smaller stage, and the B = 4096 particle
+// MLP stages, lost 10-60 % (fewer waves per SIMD to hide the weight stream).  Plain prologues only.
+#ifndef TD3_WN4X2
+#define TD3_WN4X2 1
+#endif
+#ifndef TD3_WN4X2_MIN_BLOCKS
+#define TD3_WN4X2_MIN_BLOCKS 384
+#endif
+static int gemm_wn_rows(int wn, int pro, int Bp, int wn4_blocks) {
+  const bool plain = pro == kProCopy || pro == kProLN || pro == kProLNBwd || pro == kProHeadBwd;
+  return (TD3_WN4X2 && wn == 4 && plain && Bp >= 512 && Bp <= 2048 && Bp % 64 == 0 &&
+          wn4_blocks >= TD3_WN4X2_MIN_BLOCKS) ? kWn4x2 : wn;
+}
 
 // Forward layers 0..2 of several networks (one launch per layer); layer 0 copies the
 // network input rows, layers 1 and 2 apply the previous layer's LayerNorm in the prologue.
@@ -538,16 +553,20 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     std::vector<GemmProb> probs;
     int maxKp = 0;
     int wn1_blocks = 0;
+    int wn4_blocks = 0;
     for (auto& it : items) {
       maxKp = std::max(maxKp, it.net->lin[l].Kp);
       wn1_blocks += (Bp / 32) * ((it.net->lin[l].Np + 31) / 32);
+      wn4_blocks += (Bp / 32) * ((it.net->lin[l].Np + 127) / 128);
     }
-    const int wn = gemm_wn(maxKp, Bp, wn1_blocks, true);
+    int wn = gemm_wn(maxKp, Bp, wn1_blocks, true);
     const bool lnin = items[0].net->lnin;          // TD3_particles lnorm1 on the MLP input
     const bool l0 = fuse_l0 && l == 1;             // this launch also computes layer 0
     const bool gather = ring && (l == 0 || l0);
     int pro = gather ? kProGather : l == 0 ? (lnin ? kProLN : kProCopy) : (norm ? kProLN : kProCopy);
     if (l0) pro = gather ? kProL0G : kProL0;
+    wn = gemm_wn_rows(wn, pro, Bp, wn4_blocks);
+    const int rt = wn_rt(wn);
     int blocks = 0, lds = 0;
     double flops = 0;
     for (size_t k = 0; k < items.size(); ++k) {
@@ -626,12 +645,13 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.relu = 1;
       p.ntiles = (L.Np + gemm_outw(wn) - 1) / gemm_outw(wn);
       p.tile_begin = blocks;
-      blocks += (Bp / 32) * p.ntiles;
+      blocks += (Bp / (32 * rt)) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
       // fused layer 0: + the staged input rows and (networks with a backward, norm on: l0_mfma's
       // `keep`) the H0 rows kept for the sliced store
       const bool keep_h0 = l0 && norm && it.stats;
-      lds = std::max(lds, gemm_lds_bytes(L.Kp) + (l0 ? 32 * kL0XS * 4 : 0) + (keep_h0 ? 32 * lds_stride(L.Kp) * 4 : 0));
+      lds = std::max(lds, gemm_lds_bytes(L.Kp, rt) + (l0 ? 32 * kL0XS * 4 : 0) +
+                              (keep_h0 ? 32 * lds_stride(L.Kp) * 4 : 0));
       if (l0) flops += 2.0 * Bp * it.net->lin[0].N * it.net->lin[0].K;
       probs.push_back(p);
     }
@@ -659,11 +679,15 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     double flops = 0;
     int maxKp = 0;
     int wn1_blocks = 0;
+    int wn4_blocks = 0;
     for (auto& it : items) {
       maxKp = std::max(maxKp, it.net->lin[l].Np);
       wn1_blocks += (Bp / 32) * ((it.net->lin[l].Kp + 31) / 32);
+      wn4_blocks += (Bp / 32) * ((it.net->lin[l].Kp + 127) / 128);
     }
-    const int wn = gemm_wn(maxKp, Bp, wn1_blocks, false);
+    const int pro = l < 2 ? kProLNBwd : head_bwd_scale != 0.f ? kProHeadBwd : kProCopy;
+    const int wn = gemm_wn_rows(gemm_wn(maxKp, Bp, wn1_blocks, false), pro, Bp, wn4_blocks);
+    const int rt = wn_rt(wn);
     for (size_t k = 0; k < items.size(); ++k) {
       const BwdItem& it = items[k];
       const LinearL& L = it.net->lin[l];
@@ -705,12 +729,11 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.relu = 0;
       p.ntiles = (L.Kp + gemm_outw(wn) - 1) / gemm_outw(wn);
       p.tile_begin = blocks;
-      blocks += (Bp / 32) * p.ntiles;
+      blocks += (Bp / (32 * rt)) * p.ntiles;
       flops += 2.0 * Bp * L.N * L.K;
-      lds = std::max(lds, gemm_lds_bytes(L.Np));
+      lds = std::max(lds, gemm_lds_bytes(L.Np, rt));
       probs.push_back(p);
     }
-    const int pro = l < 2 ? kProLNBwd : head_bwd_scale != 0.f ? kProHeadBwd : kProCopy;
     TD3_RC(push_gemm_stage(h, owned, st, probs, 1, wn, pro, Bp, lds, blocks,
                            flops, std::string(tag) + "_bwd" + std::to_string(l), nullptr, 0));
   }
