@@ -261,6 +261,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="halfcheetah")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dp-self", action="store_true",
+                    help="diagnostic: run the data-parallel stage lists (grad-only dW, RCCL all-reduce, "
+                         "flat Adam) on a one-rank communicator, to price the DP path without peers")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="step launch mode: hipGraph replay, direct launches, or auto (replay while the "
@@ -281,9 +284,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or args.dp_self:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from td3_amd import _lib
 
@@ -302,7 +310,7 @@ def main():
                   use_graph=use_graph, norm=None if args.norm == "none" else args.norm)
     rb = RB(obs, Box((cfg["ad"],)), max_size=REPLAY_ROWS, device=local, seed=101 + rank)
     rb.fill_synthetic(REPLAY_ROWS, cfg["ma"], seed=7 + rank)
-    if world > 1:
+    if world > 1 or args.dp_self:
         from td3_amd.data_parallel import init_rccl
         init_rccl(pol, dist)
 
@@ -373,7 +381,7 @@ def main():
                     "torch-default random init)",
             "config": {"workload": cfg["workload"],
                        "global_batch": B * world, "per_gpu_batch": B, "replay_per_gpu": REPLAY_ROWS,
-                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "parallelism": f"dp{world}" if world > 1 else ("dp1-self" if args.dp_self else "single"),
                        "global_steps_per_s": round(gsteps, 3),
                        "launch": args.launch, "norm": args.norm},
         }
