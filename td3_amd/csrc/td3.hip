@@ -491,6 +491,13 @@ static int push_row2_stage(std::vector<Stage>& st, std::vector<GemmProb>& probs,
   return 0;
 }
 
+// Planner tuning knobs read from the environment when a plan is built (A/B runs; defaults are the
+// measured best)
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atoi(e) : dflt;
+}
+
 // Output columns per GEMM workgroup.  32 (WN=1, K split 8 ways) gives the shortest MFMA chain,
 // right for most latency-bound B=256 stages.  A stage of >= 256 such workgroups is bound by the
 // A rows and weights that every 32-column tile re-reads instead:
@@ -508,8 +515,21 @@ static int push_row2_stage(std::vector<Stage>& st, std::vector<GemmProb>& probs,
 #ifndef TD3_WN0_MAX
 #define TD3_WN0_MAX 128
 #endif
-static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd) {
-  if (maxK <= 128 || (Bp >= 512 && wn1_blocks >= 256)) return 4;
+// B >= 512 stages whose 128-column split leaves the chip under-filled (fewer than TD3_WN4_MIN
+// workgroups, e.g. a one- or two-network layer: 128 of 256 CUs) take 64-column workgroups when
+// those fit about one round (<= TD3_WN2_MAXB): the prologue repeats per column tile but the MFMA
+// chain halves (the timeline: MFMA phase ~7.5 us of a 12.6 us TF_fwd2 span on 128 CUs).
+// Input-grad stages too (TD3_WN2_BWD; those paired with a forward stage in a dual launch have
+// >= 256 WN = 4 workgroups and stay at WN = 4). Humanoid 3.78 k -> 3.94 k steps/s: TF_fwd2 13.7 -> 10.8,
+// AF_fwd0 12.6 -> 9.3, AF_fwd1 15.4 -> 11.9, AQB_bwd1 14.6 -> 11.0, AB_bwd1 15.4 -> 12.5 us.
+static int gemm_wn(int maxK, int Bp, int wn1_blocks, bool fwd, int wn4_blocks = 0, int wn2_blocks = 0) {
+  if (maxK <= 128) return 4;
+  if (Bp >= 512 && wn1_blocks >= 256) {
+    static const int wn4_min = env_int("TD3_WN4_MIN", 224), wn2_maxb = env_int("TD3_WN2_MAXB", 288);
+    static const bool wn2_bwd = env_int("TD3_WN2_BWD", 1) != 0;
+    if ((fwd || wn2_bwd) && wn4_blocks > 0 && wn4_blocks < wn4_min && wn2_blocks <= wn2_maxb) return 2;
+    return 4;
+  }
   if (wn1_blocks <= TD3_WN0_MAX) return 0;
   return (fwd && wn1_blocks >= TD3_WN2_MIN) ? 2 : 1;
 }
@@ -553,13 +573,14 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     std::vector<GemmProb> probs;
     int maxKp = 0;
     int wn1_blocks = 0;
-    int wn4_blocks = 0;
+    int wn4_blocks = 0, wn2_blocks = 0;
     for (auto& it : items) {
       maxKp = std::max(maxKp, it.net->lin[l].Kp);
       wn1_blocks += (Bp / 32) * ((it.net->lin[l].Np + 31) / 32);
+      wn2_blocks += (Bp / 32) * ((it.net->lin[l].Np + 63) / 64);
       wn4_blocks += (Bp / 32) * ((it.net->lin[l].Np + 127) / 128);
     }
-    int wn = gemm_wn(maxKp, Bp, wn1_blocks, true);
+    int wn = gemm_wn(maxKp, Bp, wn1_blocks, true, wn4_blocks, wn2_blocks);
     const bool lnin = items[0].net->lnin;          // TD3_particles lnorm1 on the MLP input
     const bool l0 = fuse_l0 && l == 1;             // this launch also computes layer 0
     const bool gather = ring && (l == 0 || l0);
@@ -679,14 +700,15 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     double flops = 0;
     int maxKp = 0;
     int wn1_blocks = 0;
-    int wn4_blocks = 0;
+    int wn4_blocks = 0, wn2_blocks = 0;
     for (auto& it : items) {
       maxKp = std::max(maxKp, it.net->lin[l].Np);
       wn1_blocks += (Bp / 32) * ((it.net->lin[l].Kp + 31) / 32);
+      wn2_blocks += (Bp / 32) * ((it.net->lin[l].Kp + 63) / 64);
       wn4_blocks += (Bp / 32) * ((it.net->lin[l].Kp + 127) / 128);
     }
     const int pro = l < 2 ? kProLNBwd : head_bwd_scale != 0.f ? kProHeadBwd : kProCopy;
-    const int wn = gemm_wn_rows(gemm_wn(maxKp, Bp, wn1_blocks, false), pro, Bp, wn4_blocks);
+    const int wn = gemm_wn_rows(gemm_wn(maxKp, Bp, wn1_blocks, false, wn4_blocks, wn2_blocks), pro, Bp, wn4_blocks);
     const int rt = wn_rt(wn);
     for (size_t k = 0; k < items.size(); ++k) {
       const BwdItem& it = items[k];
@@ -792,10 +814,6 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 constexpr int kDwSplitWorkgroups = TD3_DWSK_G;   // one per CU of the MI355X
 // Matrix tile edge (64; TD3_DWSK_T=128 selects 128 x 128 tiles: slower on Humanoid, 54 vs 45 us) and the cost of a full matrix
 // step relative to a vector step (TD3_DWSK_WM, default 8): read when a plan is built, for A/B runs
-static int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e && *e ? std::atoi(e) : dflt;
-}
 static int dwsk_tile_edge() { return env_int("TD3_DWSK_T", 64) == 128 ? 128 : 64; }
 static int dwsk_matrix_weight() { return std::max(1, env_int("TD3_DWSK_WM", 8)); }
 
