@@ -134,7 +134,9 @@ def gather_line(pol, rb, cfg, reps=5, iters=40):
         F = cfg["F"]
         per_row = 3 * F + 2 * (2 * F + ad) + 2          # XA, XAQ, XTA, XQ_j [f | a], XTQ_j, r, nd (CDQ)
         read, written = B * per_row * 4, Bp * per_row * 4
-        algorithmic = B * 4 * (2 * (F + cfg["N"] * cfg["D"]) + ad + 2)
+        # what this kernel has to move: the record's small fields (f, a, f', r, nd) once each way;
+        # the particle blocks are not copied (the encoders read them from the ring in place)
+        algorithmic = B * 4 * (2 * F + ad + 2)
     else:
         sd = cfg["sd"]
         rec = (2 * sd + ad + 2 + 3) // 4 * 4
