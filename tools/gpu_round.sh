@@ -13,6 +13,10 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-m
 rc=$?; tail -4 gpurun_out/pytest_$tag.log; echo "pytest rc=$rc"
 grep -E "FAILED|ERROR" gpurun_out/pytest_$tag.log | head -20
 fatal $rc && exit $rc
+# a GPU fault leaves the context unusable: stop before the benches run into it again
+if grep -qE "illegal memory access|hipErrorIllegalAddress|Memory access fault" gpurun_out/pytest_$tag.log; then
+  echo "GPU fault in the tests: no benches"; exit 3
+fi
 for c in $cfgs; do
   case $c in
     halfcheetah) args="--steps 2000 --warmup 100";;
