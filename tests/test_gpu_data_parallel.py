@@ -107,6 +107,43 @@ def test_local_replicas_equal_global_batch_step(name, n):
         assert all(q._counters() == (L.total_it, L.critic_step, L.actor_step) for q in pols)
 
 
+def test_c5_eight_replicas_global_batch_8192():
+    """BASELINE config 5 (Humanoid-v4, 8 x MI355X, 1024 rows per GPU = global batch 8192) through
+    the product's data-parallel stage lists: 8 replicas of one process at Humanoid widths, each on
+    its 1024-row shard (split-K grad-only dW at B >= 512, the fixed-order sum in place of RCCL's
+    all-reduce, flat Adam with grad scale 1/8), against the oracle's ONE global-batch step at
+    B = 8192 (TD3_featured.py:148-164).  A critic-only and a policy step, teacher-forced."""
+    from helpers import featured_setup_dims
+    from td3_amd.data_parallel import train_local
+    n, b = 8, 1024
+    S = featured_setup_dims(376, 17, 0.4, "layer", B=n * b, steps=2)
+    pols, rbs = _replicas(S, n, _make)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    rs = np.random.RandomState(55)
+    for step in (1, 2):
+        idx = rs.randint(0, gen.BUFFER_ROWS, size=n * b)
+        noise = rs.standard_normal((n * b, S["ad"])).astype(np.float32)
+        for pol in pols:
+            _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        outs = train_local(pols, rbs, b, indices=idx.reshape(n, b), noise=noise.reshape(n, b, -1), stats=True)
+        y = np.concatenate([o["y"][:, 0] for o in outs])
+        q2 = np.concatenate([o["q2"][:, 0] for o in outs])
+        assert _rel_to_max(y, rec["y"][:, 0]) <= 1e-5, (step, "y")
+        assert _rel_to_max(q2, rec["q2"][:, 0]) <= 1e-5, (step, "q2")
+        np.testing.assert_allclose(np.mean([o["critic_loss"] for o in outs]), rec["critic_loss"], rtol=1e-5)
+        assert all(o["actor_step"] == ("actor_loss" in rec) for o in outs)
+        if "actor_loss" in rec:
+            np.testing.assert_allclose(np.mean([o["actor_loss"] for o in outs]), rec["actor_loss"],
+                                       rtol=1e-5, atol=1e-7)
+        _check_replicas_equal(pols)
+        _check_grads(pols[0], n, rec, step)
+        for grp, ref in (("critic", L.critic), ("critic_target", L.critic_target), ("actor", L.actor),
+                         ("actor_target", L.actor_target)):
+            _params_close(getattr(pols[0], grp).numpy_dict(), ref, L.lr, (step, grp), frac=0.99)
+        assert all(q._counters() == (L.total_it, L.critic_step, L.actor_step) for q in pols)
+
+
 def test_local_replicas_free_running_philox():
     """Production draws (each replica's Philox stream over its own ring, device noise): four
     free-running steps keep the replicas bit-identical although their batches differ."""
