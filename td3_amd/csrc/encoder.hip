@@ -234,6 +234,9 @@ __global__ __launch_bounds__(256) void enc_gpool_kernel(EncBwdArgs a) {
 
 // ROLE 0: role A only, 1: role B only, 2: both on every staged tile (one pass over the particles,
 // masks and pooled grads; the role B h1 recompute and dW2 MFMAs interleave with role A's chains)
+#ifndef TD3_ENC_SKEW
+#define TD3_ENC_SKEW 1
+#endif
 template <int DK, int ROLE>
 __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
   constexpr bool kA = ROLE != 1, kB = ROLE != 0;
@@ -367,12 +370,14 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
     const uint32_t rb_now = st_r;
     __syncthreads();
     if (it + 1 < ntot) fetch(it + 1);
-    {
+    auto do_a = [&]() {
       if constexpr (kA) {
         f32x16 acc;
         role_a_dh1(acc, mb, gsb);
         role_a_dw1(acc, xb, rb_now);
       }
+    };
+    auto do_b = [&]() {
       if constexpr (kB) {
         // ---- h1 of this wave's channels k_own at rows crow(r) + 4h, kept in registers as the
         // B operand: lane (i, h) of step s supplies h1[row crow(s)+4h][k_own].
@@ -421,6 +426,17 @@ __global__ __launch_bounds__(512) void enc_bwd_kernel(EncBwdArgs a) {
             for (int s = 0; s < 16; ++s) wq[s] = wn[s];
         }
       }
+    };
+    // the two waves of a SIMD (w, w + 4) run the roles in opposite order: each role is an MFMA
+    // phase and a VALU phase (A: dh1 chain, then dz1 / dW1 FMAs; B: h1 recompute, then dW2
+    // chain), so one wave's VALU phase meets the other's MFMA chain instead of both waves
+    // reaching their VALU phases together after the tile barrier
+    if (ROLE == 2 && TD3_ENC_SKEW && wave >= 4) {
+      do_b();
+      do_a();
+    } else {
+      do_a();
+      do_b();
     }
   }
   // ---- partial slab of this workgroup
