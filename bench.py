@@ -161,15 +161,40 @@ def gather_line(pol, rb, cfg, reps=5, iters=40):
                        else "fused into F_fwd01 (kProL0G); this line is the stand-alone kernel"}
 
 
-def roofline_from_stages(rows, pmc):
-    """Dominant kernel over one odd + one even step; achieved = algorithmic FLOP / time."""
+def kernel_families(rows):
+    """Stage rows of one odd + one even step grouped by the HIP kernel they launch."""
     fam = {}
     for r in rows:
         f = fam.setdefault(r["kernel"], {"ms": 0.0, "flops": 0.0, "launches": 0})
         f["ms"] += r["ms"]
         f["flops"] += r["flops"]
         f["launches"] += 1
-    dom = max((k for k in fam if k != "rccl"), key=lambda k: fam[k]["ms"])
+    return fam
+
+
+def dominant_kernel(rows):
+    fam = kernel_families(rows)
+    return max((k for k in fam if k != "rccl"), key=lambda k: fam[k]["ms"])
+
+
+def probe_kernel(pol, rb, batch, kernel, steps):
+    """The kernel's in-step device time: `steps` production steps (after the timed region) with HIP
+    events around each of its launches on the step stream (td3_probe_kernel)."""
+    lib, h = pol._lib, pol._h
+    ms, n = C.c_float(), C.c_int()
+    if lib.td3_probe_kernel(h, rb.handle, batch, kernel.encode(), steps, C.byref(ms), C.byref(n)):
+        raise RuntimeError(lib.td3_last_error().decode())
+    return {"steps": steps, "launches": n.value, "ms_total": float(ms.value)}
+
+
+def roofline_from_stages(rows, pmc, probe=None):
+    """Dominant kernel over one odd + one even step; achieved = algorithmic FLOP per launch / its
+    mean launch time in back-to-back stage replays (HIP events, handle stream: within a few % of
+    the rocprofv3 average of the same bench command).  `probe` adds the in-step figure: HIP events
+    around each launch inside production steps, which also counts the event records and the
+    launch's dispatch behind the previous stage (an upper bound on the kernel's duration)."""
+    fam = kernel_families(rows)
+    dom = dominant_kernel(rows)
     f = fam[dom]
     per_launch_flops = f["flops"] / f["launches"]
     per_launch_s = f["ms"] / f["launches"] * 1e-3
@@ -177,11 +202,24 @@ def roofline_from_stages(rows, pmc):
     traffic = None
     if pmc and dom in pmc.get("kernels", {}):
         traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
-    return {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 3),
-            "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-            "traffic": traffic, "launches_per_2_steps": f["launches"],
-            "avg_launch_us": round(per_launch_s * 1e6, 3),
-            "flops_per_launch": per_launch_flops}, fam
+    out = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 3),
+           "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+           "traffic": traffic, "launches_per_2_steps": f["launches"],
+           "avg_launch_us": round(per_launch_s * 1e6, 3),
+           "flops_per_launch": per_launch_flops,
+           "timing": "back-to-back replays of the stage (td3_time_stage, HIP events on the handle stream)"}
+    if dom.startswith("td3::dwsk_kernel"):
+        out["stage_kernels"] = [dom, "td3::dwsk_combine_kernel"]
+        out["timing"] += ("; the split-K dW stage is two launches (partial tiles, then the fixed-order "
+                          "combine with Adam), timed together and charged with the stage's FLOPs")
+    if probe and probe["launches"] > 0:
+        in_step_s = probe["ms_total"] / probe["launches"] * 1e-3
+        out["in_step_launch_us"] = round(in_step_s * 1e6, 3)
+        out["in_step_frac"] = round(per_launch_flops / in_step_s / 1e12 / FP32_PEAK_TFLOPS, 4)
+        out["in_step_timing"] = (f"HIP events around each of the stage's {probe['launches']} launches in "
+                                 f"{probe['steps']} production steps right after the timed region "
+                                 "(td3_probe_kernel); includes the event records and the dispatch gap")
+    return out, fam
 
 
 def _cpu_model():
@@ -344,13 +382,14 @@ def main():
         rows = stage_table(pol, rb, B, iters=50 if cfg["kind"] != "particles" else 3,
                            reps=5 if cfg["kind"] != "particles" else 1)
         gat = gather_line(pol, rb, cfg)
+        probe = probe_kernel(pol, rb, B, dominant_kernel(rows), 200 if cfg["kind"] != "particles" else 4)
         if rank == 0:
             pmc = None
             pmc_path = os.path.join(ROOT, "profiles", PMC_FILES.get(args.config, ""))
             if os.path.isfile(pmc_path) and args.norm == "layer":
                 with open(pmc_path) as f:
                     pmc = json.load(f)
-            roof, fam = roofline_from_stages(rows, pmc)
+            roof, fam = roofline_from_stages(rows, pmc, probe)
             if roof.get("traffic") is not None:
                 roof["traffic_source"] = (f"profiles/{PMC_FILES[args.config]}: rocprofv3 --pmc FETCH_SIZE / "
                                           "WRITE_SIZE of this kernel in a separate profiling run of this "

@@ -233,6 +233,12 @@ const char* td3_stage_kernel(td3_handle* h, int i);
  * two HIP events on the handle stream, after one full step at `batch`); returns mean ms per
  * launch.  Stage 0 is the stand-alone replay-ring gather (gather_kernel) of the profiled ring. */
 int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean);
+/* Run `steps` production training steps (Philox draws from rb, direct launches) with every launch
+ * of the HIP kernel `kernel` (a td3_stage_kernel name) between two HIP events on the step stream:
+ * the kernel's in-step device time, summed over its `launches`.  Real steps: counters and
+ * parameters advance. */
+int td3_probe_kernel(td3_handle* h, rb_handle* rb, int batch, const char* kernel, int steps, float* ms_total,
+                     int* launches);
 /* Algorithmic FLOPs of one launch of stage i (MFMA stages; 0 otherwise). */
 double td3_stage_flops(td3_handle* h, int i);
 

@@ -332,6 +332,12 @@ struct td3_handle {
   int nranks = 1, rank = 0;
   std::vector<Stage>* last_body = nullptr;
   Ring* last_ring = nullptr;                  // the ring of the last td3_profile_stages (stage 0: its gather)
+  // td3_probe_kernel: while set, steps launch directly and every stage launching `probe_kernel` is
+  // bracketed by a pair of HIP events on the step's stream (probe_ev[2k], probe_ev[2k + 1])
+  bool probing = false;
+  std::string probe_kernel;
+  std::vector<hipEvent_t> probe_ev;
+  int probe_used = 0;
   std::vector<std::string> stage_names;
   std::vector<std::string> stage_kernels;
 };
@@ -1780,6 +1786,27 @@ static int run_stages(std::vector<Stage>& st, hipStream_t s) {
   return 0;
 }
 
+// run_stages with the probed kernel's launches between two events each (td3_probe_kernel)
+static int run_stages_probed(td3_handle* h, std::vector<Stage>& st, hipStream_t s) {
+  for (auto& x : st) {
+    const bool hit = x.kernel == h->probe_kernel;
+    if (hit) {
+      while ((int)h->probe_ev.size() < h->probe_used + 2) {
+        hipEvent_t e;
+        TD3_HIP(hipEventCreate(&e));
+        h->probe_ev.push_back(e);
+      }
+      TD3_HIP(hipEventRecord(h->probe_ev[h->probe_used], s));
+    }
+    TD3_RC(x.run(s));
+    if (hit) {
+      TD3_HIP(hipEventRecord(h->probe_ev[h->probe_used + 1], s));
+      h->probe_used += 2;
+    }
+  }
+  return 0;
+}
+
 // Input stage: Philox index draw + gather from the ring into the padded batch buffers.
 static int input_from_ring_particles(td3_handle* h, Ring* r, Plan* P, bool inject_idx, hipStream_t s);
 
@@ -1887,12 +1914,12 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
   // asking the stream queues a marker, a per-step drain) training launches directly.
   // Data parallel (RCCL comm attached): auto launches directly, so every rank issues its
   // all-reduces the same way whatever its local progress (no captured / uncaptured mix).
-  const bool graph = h->cfg.use_graph == 1 ||
-                     (h->cfg.use_graph == 2 && !h->comm && !actor_phase && h->act_used &&
-                      hipEventQuery(h->actor_ev) != hipErrorNotReady);
+  const bool graph = !h->probing && (h->cfg.use_graph == 1 ||
+                                      (h->cfg.use_graph == 2 && !h->comm && !actor_phase && h->act_used &&
+                                       hipEventQuery(h->actor_ev) != hipErrorNotReady));
   if (!graph) {
     if (ring && !fused) TD3_RC(input_from_ring(h, ring, P, false, s));
-    return run_stages(st, s);
+    return h->probing ? run_stages_probed(h, st, s) : run_stages(st, s);
   }
   // graphs bake the ring in (records, d_size, seed, record width): a ring allocated since —
   // even at the same address, e.g. after ReplayBuffer.load() — is captured again
@@ -3081,6 +3108,37 @@ const char* td3_stage_kernel(td3_handle* h, int i) {
 double td3_stage_flops(td3_handle* h, int i) {
   if (!h || !h->last_body || i <= 0 || i > (int)h->last_body->size()) return 0.0;
   return (*h->last_body)[i - 1].flops;
+}
+
+int td3_probe_kernel(td3_handle* h, rb_handle* rb, int batch, const char* kernel, int steps, float* ms_total,
+                     int* launches) {
+  TD3_ARG(h && rb && kernel && ms_total && launches, "null argument");
+  TD3_ARG(steps > 0, "steps must be positive");
+  TD3_ARG(!h->local, "a td3_comm_init_local replica steps through td3_train_step_local only");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  h->probing = true;
+  h->probe_kernel = kernel;
+  h->probe_used = 0;
+  int rc = 0;
+  for (int i = 0; i < steps && rc == 0; ++i) rc = td3_train_step(h, rb, batch, nullptr, nullptr, nullptr, nullptr);
+  h->probing = false;
+  if (rc == 0) rc = td3_sync(h);
+  float total = 0.f;
+  for (int k = 0; rc == 0 && k + 1 < h->probe_used; k += 2) {
+    float ms = 0.f;
+    const hipError_t e = hipEventElapsedTime(&ms, h->probe_ev[k], h->probe_ev[k + 1]);
+    if (e != hipSuccess) {
+      set_error("td3_probe_kernel: hipEventElapsedTime: %s", hipGetErrorString(e));
+      rc = -2;
+    }
+    total += ms;
+  }
+  for (hipEvent_t e : h->probe_ev) (void)hipEventDestroy(e);
+  h->probe_ev.clear();
+  *ms_total = total;
+  *launches = h->probe_used / 2;
+  h->probe_used = 0;
+  return rc;
 }
 
 int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean) {
