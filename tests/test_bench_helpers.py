@@ -1,0 +1,59 @@
+"""bench.py's accounting on CPU (no GPU): the roofline object of the dominant kernel, the in-step
+probe fields, the split-K dW stage note, and the step FLOP model against SURVEY.md §8d."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _rows():
+    # one odd + one even step: F_fwd01 twice (dominant), a row kernel, the dW stage
+    return [
+        dict(phase=0, stage="F_fwd01", kernel="td3::gemm_kernel<0, 2, 5>", ms=0.016, flops=3.5e8),
+        dict(phase=0, stage="heads", kernel="td3::row_kernel2<0, 7, true>", ms=0.005, flops=0.0),
+        dict(phase=1, stage="F_fwd01", kernel="td3::gemm_kernel<0, 2, 5>", ms=0.017, flops=4.0e8),
+        dict(phase=1, stage="C_dw", kernel="td3::dw_kernel<true>", ms=0.011, flops=3.0e8),
+    ]
+
+
+def test_roofline_dominant_kernel_and_fraction():
+    roof, fam = bench.roofline_from_stages(_rows(), None)
+    assert roof["kernel"] == "td3::gemm_kernel<0, 2, 5>"
+    assert roof["launches_per_2_steps"] == 2
+    assert roof["avg_launch_us"] == pytest.approx(16.5)
+    assert roof["flops_per_launch"] == pytest.approx(3.75e8)
+    assert roof["achieved"] == pytest.approx(3.75e8 / 16.5e-6 / 1e12, rel=1e-3)
+    assert roof["frac"] == pytest.approx(roof["achieved"] / bench.FP32_PEAK_TFLOPS, abs=1e-4)
+    assert roof["traffic"] is None and "stage_kernels" not in roof
+    assert set(fam) == {"td3::gemm_kernel<0, 2, 5>", "td3::row_kernel2<0, 7, true>", "td3::dw_kernel<true>"}
+
+
+def test_roofline_in_step_probe_fields_and_traffic():
+    pmc = {"kernels": {"td3::gemm_kernel<0, 2, 5>": {"hbm_bytes_per_launch": 9491019}}}
+    probe = {"steps": 200, "launches": 200, "ms_total": 4.0}
+    roof, _ = bench.roofline_from_stages(_rows(), pmc, probe)
+    assert roof["traffic"] == 9491019
+    assert roof["in_step_launch_us"] == pytest.approx(20.0)
+    assert roof["in_step_frac"] == pytest.approx(3.75e8 / 20e-6 / 1e12 / bench.FP32_PEAK_TFLOPS, abs=1e-4)
+    assert roof["avg_launch_us"] == pytest.approx(16.5)          # achieved stays on the replays
+
+
+def test_split_k_dw_stage_is_named_as_two_launches():
+    rows = [dict(phase=0, stage="C_dw", kernel="td3::dwsk_kernel<true, false>", ms=0.044, flops=1.95e9)]
+    roof, _ = bench.roofline_from_stages(rows, None)
+    assert roof["stage_kernels"] == ["td3::dwsk_kernel<true, false>", "td3::dwsk_combine_kernel"]
+
+
+def test_rccl_stage_is_never_the_dominant_kernel():
+    rows = _rows() + [dict(phase=0, stage="C_allreduce", kernel="rccl", ms=1.0, flops=0.0)]
+    assert bench.dominant_kernel(rows) == "td3::gemm_kernel<0, 2, 5>"
+
+
+@pytest.mark.parametrize("name,gflop", [("halfcheetah", 1.753), ("humanoid", 10.416), ("particles", 1126.3)])
+def test_step_flops_match_survey(name, gflop):
+    assert bench.step_flops(bench.CONFIGS[name]) / 1e9 == pytest.approx(gflop, rel=1e-3)
