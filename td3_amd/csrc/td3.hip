@@ -819,9 +819,9 @@ static int add_bwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
 #endif
 constexpr int kDwSplitWorkgroups = TD3_DWSK_G;   // one per CU of the MI355X
 // Matrix tile edge (64; TD3_DWSK_T=128 selects 128 x 128 tiles: slower on Humanoid, 54 vs 45 us) and the cost of a full matrix
-// step relative to a vector step (TD3_DWSK_WM, default 8): read when a plan is built, for A/B runs
+// step relative to a vector step (TD3_DWSK_WM, default 6: Humanoid A_dw 28.0 -> 26.2 us, particles C_dw 105 -> 97 us against 8): read when a plan is built, for A/B runs
 static int dwsk_tile_edge() { return env_int("TD3_DWSK_T", 64) == 128 ? 128 : 64; }
-static int dwsk_matrix_weight() { return std::max(1, env_int("TD3_DWSK_WM", 8)); }
+static int dwsk_matrix_weight() { return std::max(1, env_int("TD3_DWSK_WM", 6)); }
 
 // Weight / bias / LN grads of every layer of `items`, fused with the optimizer.
 // enc (TD3_particles): the encoder partial slabs of `items` (reduced + optimizer in one launch).
