@@ -692,8 +692,9 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
   // dependent kernel-argument round trips between the row's loads)
   asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]),
                "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.ex[11]),
-               "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[2]), "s"(P.exi[3]), "s"(P.exi[4]), "s"(P.exi[5]),
-               "s"(P.exi[6]), "s"(P.exi[7]), "s"(P.exf[0]), "s"(P.Aout), "s"(P.ldao), "s"(P.B));
+               "s"(P.ex[12]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[2]), "s"(P.exi[3]), "s"(P.exi[4]),
+               "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.exi[7]), "s"(P.exi[8]), "s"(P.exf[0]), "s"(P.Aout),
+               "s"(P.ldao), "s"(P.B));
   const int K0 = P.exi[0], ld0 = P.exi[1], ldw1 = P.exi[2], sd = P.exi[3], ad = P.exi[4];
   const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
   const float ma = P.exf[0];
@@ -714,7 +715,15 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
     rs0[0] = rs3[0] = 1.f;
   }
   const float tl = c.lane < ad ? gld(P.ex[5] + ((size_t)c.row * 32 + c.lane)) : 0.f;
-  head_cols(P.ex[4], ldw1, sd, ad, c.lane, w1);        // W1[:, sd+o]: the action columns
+  // W1[:, sd+o], the action columns: rows of the transposed copy when the step keeps one (ex[12],
+  // row length exi[8]: coalesced, the same elements per lane), else strided column reads
+  const float* w1t = P.ex[12];
+  if (w1t) {
+#pragma unroll
+    for (int o = 0; o < kHeadRegs; ++o) rv_load(w1[o], w1t + (size_t)(o < ad ? o : 0) * P.exi[8], K0, c.lane);
+  } else {
+    head_cols(P.ex[4], ldw1, sd, ad, c.lane, w1);
+  }
 #pragma unroll
   for (int o = 0; o < kHeadRegs; ++o) {
     const int oo = o < ad ? o : 0;
@@ -742,7 +751,13 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
   // columns and W4 rows requested in one batch (one load round trip per block, not per output)
   for (int ob = kHeadRegs; ob < ad; ob += kHeadRegs) {
     float w1b[kHeadRegs][8], w4b[kHeadRegs][8];
-    head_cols(P.ex[4], ldw1, sd + ob, ad - ob, c.lane, w1b);
+    if (w1t) {
+#pragma unroll
+      for (int o = 0; o < kHeadRegs; ++o)
+        rv_load(w1b[o], w1t + (size_t)(ob + o < ad ? ob + o : 0) * P.exi[8], K0, c.lane);
+    } else {
+      head_cols(P.ex[4], ldw1, sd + ob, ad - ob, c.lane, w1b);
+    }
 #pragma unroll
     for (int o = 0; o < kHeadRegs; ++o) {
       const int oo = ob + o < ad ? ob + o : 0;
@@ -1459,6 +1474,20 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
         if (MODE == 0 && P.bias) v = v + bias;
         if (P.relu) v = fmaxf(v, 0.f);
         if (n0 + colw < P.Nout) gst(P.C + ((size_t)(m0 + rt * 32 + row) * P.ldc + n0 + colw), v);
+      }
+    }
+  }
+  // a separate layer-0 forward stage of the actor phase (td3.hip W1aT): the workgroups of column
+  // tile nt also write its weight rows' columns [exi[10], exi[10] + exi[11]), transposed, for
+  // actor_head_bwd -- row n0 + r by row tile r % mtiles (done by row tile 0 alone, the copy was
+  // that workgroup's tail: AF_fwd0 +0.9 us)
+  if constexpr (MODE == 0 && PRO == kProCopy) {
+    float* tc = P.ex[12];
+    if (tc) {
+      const int tcol = P.exi[10], tn = P.exi[11];
+      for (int e = threadIdx.x; e < OUTW * tn; e += NT) {
+        const int r = e / tn, o = e % tn, n = n0 + r;
+        if (r % mtiles == mt && n < P.Nout) gst(tc + ((size_t)o * P.Nout + n), gld(P.W + ((size_t)n * P.ldw + tcol + o)));
       }
     }
   }

@@ -206,6 +206,10 @@ struct Plan {
   int ld_sa = 0;
   float *R = nullptr, *ND = nullptr, *noise = nullptr, *Y = nullptr, *sqerr = nullptr;
   float* gscale[2] = {};                // [Bp] g_r = 2/B (Q_j,r - y_r): row scale of Q_j's unit backward
+  // Q1's layer-0 action columns transposed, [ad][Np0] (W1[:, sd + o] as row o), written by the actor
+  // phase's separate layer-0 stage (AF_fwd0) for actor_head_bwd's coalesced reads; null when layer 0
+  // is fused into the layer-1 launch (those rows are 32 floats: the strided reads cost nothing)
+  float* W1aT = nullptr;
   int64_t* d_idx = nullptr;
   int64_t* d_inject_idx = nullptr;
   EvalB TA, Q[2], A, TQ[2], AQ;
@@ -398,6 +402,10 @@ struct RingOut {
 struct FwdItem {
   const NetL* net; const float* P; EvalB* e; bool store_u; bool stats;
   int ring_src = -1;      // layer 0 read from the replay ring (kProGather): record offset of the input
+  // separate layer-0 stage only: columns [tcol, tcol + tn) of the layer-0 weight, transposed into
+  // tcopy [tn][Np0] by the stage's first row tile (GemmProb ex[12] / exi[10] / exi[11])
+  float* tcopy = nullptr;
+  int tcol = 0, tn = 0;
 };
 struct BwdItem { const NetL* net; const float* P; EvalB* e; bool store_dz; };
 
@@ -626,6 +634,11 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
             p.ldao = L.Kp;
           }
         }
+      }
+      if (l == 0 && !l0 && !gather && !lnin && it.tcopy) {
+        p.ex[12] = it.tcopy;
+        p.exi[10] = it.tcol;
+        p.exi[11] = it.tn;
       }
       if (gather && !l0) {
         TD3_ARG(it.ring_src >= 0 && !lnin && ro, "internal: ring-sampled layer without a record field");
@@ -1095,7 +1108,7 @@ static int build_step(td3_handle* h, int B) {
   const NetL& an = h->actor.nets[0];
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[1];
-  size_t floats = (size_t)Bp * 3 * P->ld_sa + 10 * (size_t)Bp + (size_t)Bp * ad + 4096;
+  size_t floats = (size_t)Bp * 3 * P->ld_sa + 10 * (size_t)Bp + (size_t)Bp * ad + 4096 + (size_t)ad * q1.lin[0].Np;
   floats += eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, true, norm) +
             eval_floats(an, Bp, true, norm) + 2 * eval_floats(q1, Bp, false, norm) +
             eval_floats(q1, Bp, true, norm) + 1024;
@@ -1119,6 +1132,7 @@ static int build_step(td3_handle* h, int B) {
   P->d_inject_idx = (int64_t*)S.take(2 * (size_t)Bp);
   P->gscale[0] = S.take(Bp);
   P->gscale[1] = S.take(Bp);
+  P->W1aT = S.take((size_t)ad * q1.lin[0].Np);
   alloc_eval(S, an, Bp, P->X_S2A, P->ld_sa, false, norm, false, P->TA);
   alloc_eval(S, q1, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[0]);
   alloc_eval(S, q2, Bp, P->X_SA, P->ld_sa, true, norm, true, P->Q[1]);
@@ -1340,6 +1354,12 @@ static int build_step(td3_handle* h, int B) {
       if (!actor_phase) continue;
       // ---------------- delayed policy update (TD3_featured.py:156-171)
       std::vector<FwdItem> f3 = {{&q1, Pq1, &P->AQ, false, true}};
+      const bool w1at = !can_fuse_l0(f3);        // layer 0 is its own stage: it writes W1aT
+      if (w1at) {
+        f3[0].tcopy = P->W1aT;
+        f3[0].tcol = sd;
+        f3[0].tn = ad;
+      }
       TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0, nullptr, nullptr, 0, true));
       // the actor loss -mean Q1(s, pi(s)) (:159): Q1's head and its backward are the prologue of
       // AQB_bwd2 (kProHeadBwd; the row launch kRowActorLoss is the particle path's)
@@ -1361,8 +1381,10 @@ static int build_step(td3_handle* h, int B) {
         p.ex[9] = const_cast<float*>(Pa + an.ln[2].offg);
         p.ex[10] = P->A.GZ[3];
         p.ex[11] = P->A.GU[2];
+        p.ex[12] = w1at ? P->W1aT : nullptr;      // the action columns as rows (AF_fwd0 wrote them)
         p.Aout = P->A.GZ[2];
         p.ldao = an.lin[2].Np;
+        p.exi[8] = q1.lin[0].Np;
         p.exi[0] = q1.lin[0].N;
         p.exi[1] = q1.lin[0].Np;
         p.exi[2] = q1.lin[0].Kp;
