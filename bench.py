@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
 """TD3 gradient-steps/s on MI355X (BASELINE.json metric), HalfCheetah-v4 shapes, batch 256/GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--runs R] [--config C]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+``--gpus N`` without an external launcher starts the N rank processes itself (``launch_workers``,
+before any GPU call); under ``torch.distributed.run`` it must equal WORLD_SIZE.
 
 One "step" = one ``TD3.train(replay_buffer, 256)`` call (TD3_featured.py:123-171): Philox
 index draw + HBM gather from a 1e6-row replay ring pre-filled with synthetic transitions
 (SURVEY.md §8d), the twin-critic update and, every policy_freq=2 steps, the actor update +
 Polyak.  N GPUs = data parallel: every rank owns a replay shard and samples its own 256
-rows; gradients are all-reduced over RCCL (xGMI) before Adam.  ``value`` counts
-batch-256 gradient steps over all ranks (weak scaling).
+rows; gradients are all-reduced over RCCL (xGMI) before Adam, so one step is one optimizer step
+on a global batch of 256·N rows.  ``value`` = optimizer steps/s (the median of ``--runs`` timed
+runs of K steps), ``samples_per_s`` = rows consumed per second over all ranks (weak scaling).
 
 Prints ONE JSON line on rank 0 (the driver contract) with a ``roofline`` object for the
 dominant kernel (HIP-event timed live; ``step_frac`` = the step's algorithmic FLOP / measured
@@ -33,10 +37,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-# BASELINE.json configs besides the headline one (``--config``): C3 Humanoid-v4 TD3_featured
+# BASELINE.json configs besides the headline one (``--config``): C1 Pendulum-v1 (the reference's
+# CPU-runnable case) B=256 replay 1e5, C3 Humanoid-v4 TD3_featured
 # B=1024 replay 2e6, C4 water-pouring particles TD3_particles B=4096 (F=7, N=350, D=9, A=3 as
 # assumed in SURVEY.md §8d) replay 1e5.
 CONFIGS = {
+    "pendulum": dict(kind="featured", sd=3, ad=1, ma=2.0, batch=256, replay=100_000,
+                     workload="TD3_base/TD3_featured.train(replay_buffer, 256) on Pendulum-v1 shapes "
+                              "(state 3, action 1, max_action 2, actor 500-400-300, critic 2x 500-400-200, "
+                              "LayerNorm, policy_freq 2), replay 1e5 per GPU (BASELINE config 1)"),
     "halfcheetah": dict(kind="featured", sd=17, ad=6, ma=1.0, batch=256, replay=1_000_000,
                         workload="TD3_featured.train(replay_buffer, 256) on HalfCheetah-v4 shapes "
                                  "(state 17, action 6, actor 500-400-300, critic 2x 500-400-200, "
@@ -294,11 +303,15 @@ def cpu_baseline(cfg, seconds=12.0):
             "sample": f"{steps} torch-CPU train steps ({what}, B={B}, norm=layer, warm) in {dt:.1f} s"}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node, one rank each (default 1; under an external launcher "
+                         "it must equal WORLD_SIZE)")
+    ap.add_argument("--steps", type=int, default=2000, help="steps per timed run")
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--runs", type=int, default=5,
+                    help="timed runs of --steps steps each; value = their median (SURVEY.md §8d)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="halfcheetah")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dp-self", action="store_true",
@@ -311,7 +324,90 @@ def main():
     ap.add_argument("--eager", action="store_true", help="same as --launch eager")
     ap.add_argument("--norm", choices=["layer", "none", "weight_normalization"], default="layer",
                     help="network normalisation (SURVEY §8d measures norm=layer; featured configs only)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(argv, n, worker=None, grace_s=20.0):
+    """``bench.py --gpus N`` without an external launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1)
+    before this process touches the GPU -- it never imports torch -- and forward rank 0's
+    stdout (the one JSON line).  Other ranks' stdout goes to stderr.  When a rank fails, the
+    others are terminated (they would wait in a collective) and the launcher returns that rank's
+    exit status; 0 only when every rank succeeded.  ``worker`` replaces the child command
+    (CPU tests)."""
+    import signal
+    import subprocess
+    import threading
+    port = _free_port()
+    cmd = list(worker) if worker is not None else [sys.executable, os.path.abspath(__file__), *argv]
+    procs, out0 = [], []
+    for rank in range(n):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL peer buffers)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if rank == 0 else sys.stderr,
+                                      start_new_session=True))
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad and failed is None:
+            failed = bad[0]
+            print(f"bench: rank {failed[0]} exited with {failed[1]}; stopping the other ranks",
+                  file=sys.stderr, flush=True)
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGTERM)
+            deadline = time.time() + grace_s
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+            break
+        if all(c is not None for c in codes):
+            break
+        time.sleep(0.05)
+    reader.join(timeout=10)
+    text = out0[0].decode(errors="replace") if out0 and out0[0] else ""
+    if text:
+        sys.stdout.write(text)
+        sys.stdout.flush()
+    if failed is not None:
+        return failed[1] if failed[1] > 0 else 1
+    return 0
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ:
+        if (args.gpus or 1) > 1:
+            return launch_workers(sys.argv[1:] if argv is None else list(argv), args.gpus)
+        args.gpus = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus is None:
+            args.gpus = world
+        if args.gpus != world:
+            print(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
+                  file=sys.stderr)
+            return 2
+    run_rank(args)
+    return 0
+
+
+def run_rank(args):
     cfg = CONFIGS[args.config]
     if args.eager:
         args.launch = "eager"
@@ -333,7 +429,7 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from td3_amd import _lib
+    from td3_amd import _lib  # noqa: F401
 
     torch.manual_seed(1000)                         # same init on every rank
     if cfg["kind"] == "particles":
@@ -363,19 +459,23 @@ def main():
 
     for _ in range(args.warmup):
         pol.train(rb, B)
-    barrier_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pol.train(rb, B)
-    pol.sync()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    runs = []
+    for _ in range(max(1, args.runs)):
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pol.train(rb, B)
+        pol.sync()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist is not None:                       # the slowest rank's clock
+            tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        runs.append(dt)
+    dt = float(np.median(runs))
 
     rows, fam, roof, gat = None, None, None, None
     if not args.no_roofline:           # every rank runs it: profiled steps contain collectives
@@ -404,47 +504,60 @@ def main():
         cpu = cpu_baseline(cfg)
 
     if rank == 0:
-        gsteps = args.steps / dt
-        value = world * gsteps
-        metric = "TD3 gradient-steps/sec @ batch 256, HalfCheetah-v4, 1/2/4/8 GPU"
-        if args.config != "halfcheetah":
-            metric = f"TD3 gradient-steps/sec @ batch {B}, {args.config}, 1/2/4/8 GPU"
-        out = {
-            "metric": metric,
-            "value": round(value, 3),
-            "unit": "grad-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (replay ring pre-filled on device: states / particles ~ N(0,1), "
-                    "a ~ U(-max_action, max_action), r ~ N(0,1), not_done ~ Bernoulli(0.99); "
-                    "torch-default random init)",
-            "config": {"workload": cfg["workload"],
-                       "global_batch": B * world, "per_gpu_batch": B, "replay_per_gpu": REPLAY_ROWS,
-                       "parallelism": f"dp{world}" if world > 1 else ("dp1-self" if args.dp_self else "single"),
-                       "global_steps_per_s": round(gsteps, 3),
-                       "launch": args.launch, "norm": args.norm},
-        }
-        if roof is not None:
-            flops = step_flops(cfg)
-            roof["step_flops"] = flops
-            roof["step_frac"] = round(flops / (dt / args.steps) / (FP32_PEAK_TFLOPS * 1e12), 4)
-            out["roofline"] = roof
-        if gat is not None:
-            out["gather"] = gat
-            out["stage_us"] = {f"{r['phase']}:{r['stage']}": round(r["ms"] * 1e3, 2) for r in rows}
-        if cpu is not None:
-            out["cpu_baseline"] = cpu
-        print(json.dumps(out), flush=True)
+        print(json.dumps(result_line(args, cfg, world, dt, runs, roof, gat, rows, cpu)), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
 
+def result_line(args, cfg, world, dt, runs, roof=None, gat=None, rows=None, cpu=None):
+    """The driver's JSON line.  ``value`` = optimizer steps/s of the job: every rank takes the same
+    step at once (the replicas all-reduce one global batch of B·world rows per step), so this is
+    the TD3 gradient-step rate (TD3_featured.py:123-171: one ``train`` = one step) at the global
+    batch in ``config``; the rows consumed are ``samples_per_s``.  ``dt`` is the median of the timed
+    runs (the slowest rank's clock in each)."""
+    B = cfg["batch"]
+    steps_s = args.steps / dt
+    metric = "TD3 gradient-steps/sec @ batch 256, HalfCheetah-v4, 1/2/4/8 GPU"
+    if args.config != "halfcheetah":
+        metric = f"TD3 gradient-steps/sec @ batch {B}, {args.config}, 1/2/4/8 GPU"
+    out = {
+        "metric": metric,
+        "value": round(steps_s, 3),
+        "unit": "grad-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (replay ring pre-filled on device: states / particles ~ N(0,1), "
+                "a ~ U(-max_action, max_action), r ~ N(0,1), not_done ~ Bernoulli(0.99); "
+                "torch-default random init)",
+        "config": {"workload": cfg["workload"],
+                   "global_batch": B * world, "per_gpu_batch": B, "replay_per_gpu": cfg["replay"],
+                   "parallelism": f"dp{world}" if world > 1 else ("dp1-self" if args.dp_self else "single"),
+                   "launch": args.launch, "norm": args.norm},
+        "samples_per_s": round(steps_s * B * world, 1),
+        "runs": [round(args.steps / r, 3) for r in runs],
+        "value_is": f"median of {len(runs)} timed runs of {args.steps} steps each; one step = one "
+                    f"optimizer step of every rank on a global batch of {B}x{world} rows",
+    }
+    if roof is not None:
+        flops = step_flops(cfg)
+        roof["step_flops"] = flops
+        roof["step_frac"] = round(flops / (dt / args.steps) / (FP32_PEAK_TFLOPS * 1e12), 4)
+        out["roofline"] = roof
+    if gat is not None:
+        out["gather"] = gat
+    if rows is not None:
+        out["stage_us"] = {f"{r['phase']}:{r['stage']}": round(r["ms"] * 1e3, 2) for r in rows}
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    return out
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -206,7 +206,10 @@ int td3_eval_q_particles(td3_handle* h, const float* feat, const float* part, co
 
 /* ------------------------------------------------------------------ multi-GPU (RCCL) */
 int td3_comm_unique_id(unsigned char out[128]);
-/* Data-parallel mode: grads are all-reduced (sum, then /world) over RCCL before Adam. */
+/* Data-parallel mode: grads are all-reduced (sum, then /world) over RCCL before Adam.  Every
+ * call that steps the learner is then COLLECTIVE: td3_train_step / td3_train_step_batch and
+ * td3_actor_learn_particles must be made by every rank in the same order (each issues the
+ * phase all-reduces). */
 int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int rank);
 /* Test seam of the same data-parallel path inside ONE process (RCCL cannot put two ranks on one
  * GPU): the n handles (same configuration and device) become the ranks 0..n-1 of a group whose

@@ -495,10 +495,12 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   const bool target = P.exi[8] != 0;
   const float ma = P.exf[0];
   const bool gen = target && P.exi[4];
-  // the counter by an asm load into VGPRs (ctr is always set, td3.hip): a plain load of this
-  // uniform value is copied to SGPRs at once, i.e. waited for ahead of the row's loads
-  uint64_t stepv;
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(stepv) : "v"(&P.ctr->total_it) : "memory");
+  // the counter (ctr is always set, td3.hip) by an ordinary relaxed load whose address carries a
+  // lane-dependent zero (mbcnt with an empty mask): a divergent load, so the value lands in VGPRs
+  // and the compiler's own wait placement defers it to the Philox draw.  Left uniform, it is a
+  // scalar load waited for ahead of the row's loads.
+  const int64_t* ctrp = &P.ctr->total_it + __builtin_amdgcn_mbcnt_lo(0u, 0u);
+  const uint64_t stepv = (uint64_t)__hip_atomic_load(ctrp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float x[1][8], g[8], bb[8], mean[1], rstd[1];
   float w4[kHeadRegs][8], b4v[kHeadRegs];
   rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
@@ -549,7 +551,6 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   if (target) {
     float z = nz;
     if (gen) {                                               // Philox N(0,1) (randn_like, :132)
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(stepv) :: "memory");
       float g4[4];
       philox_normal4(P.seed, stepv, kStreamNoise, (uint32_t)(c.row * 8 + (o >> 2)), g4);
       z = g4[o & 3];

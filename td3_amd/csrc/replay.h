@@ -56,6 +56,8 @@ int ring_end_read(Ring* r, hipStream_t s);
 // A stream that is about to be destroyed (synchronised by the caller) stops being a ring's
 // noted reader / writer.
 void ring_forget_stream(hipStream_t s);
+// True while `r` is a live ring of allocation generation `gen` (not destroyed, not reused).
+bool ring_alive(const Ring* r, uint64_t gen);
 
 // One gather destination: rows [0, Bp) of dst[r*ld + col + c] = record[src + c], c < len.
 struct GatherSeg {

@@ -201,6 +201,11 @@ int ring_end_read(Ring* r, hipStream_t s) {
   return 0;
 }
 
+bool ring_alive(const Ring* r, uint64_t gen) {
+  std::lock_guard<std::mutex> lk(g_rings_mu);
+  return r && g_rings.count(const_cast<Ring*>(r)) && r->gen == gen;
+}
+
 }  // namespace td3
 
 using namespace td3;

@@ -336,6 +336,7 @@ struct td3_handle {
   int nranks = 1, rank = 0;
   std::vector<Stage>* last_body = nullptr;
   Ring* last_ring = nullptr;                  // the ring of the last td3_profile_stages (stage 0: its gather)
+  uint64_t last_ring_gen = 0;                 // its Ring::gen (td3_time_stage refuses a destroyed ring)
   // td3_probe_kernel: while set, steps launch directly and every stage launching `probe_kernel` is
   // bracketed by a pair of HIP events on the step's stream (probe_ev[2k], probe_ev[2k + 1])
   bool probing = false;
@@ -1980,6 +1981,9 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
 static int build_step_particles(td3_handle* h, int B);
 
 static int build_plan(td3_handle* h, int B) {
+  // the profiled stage list lives in the plan being replaced
+  h->last_body = nullptr;
+  h->last_ring = nullptr;
   return h->particles ? build_step_particles(h, B) : build_step(h, B);
 }
 
@@ -2847,6 +2851,7 @@ int td3_actor_learn_particles(td3_handle* h, const float* feat, const float* par
                               double* actor_loss) {
   TD3_ARG(h != nullptr, "null handle");
   TD3_ARG(h->particles, "td3_actor_learn_particles on a featured learner (TD3_featured has no _actor_learn)");
+  TD3_ARG(!h->local, "a td3_comm_init_local replica steps through td3_train_step_local only");
   TD3_ARG(feat && part, "null input");
   TD3_ARG(batch > 0, "batch must be positive");
   TD3_HIP(hipSetDevice(h->cfg.device));
@@ -3005,6 +3010,7 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
     td3_handle* h = hs[k];
     Ring* r = reinterpret_cast<Ring*>(rbs[k]);
     TD3_ARG(r->sd == h->sd && r->ad == h->ad && r->particles == h->particles, "replay buffer does not match");
+    TD3_ARG(!r->particles || (r->N == h->N && r->D == h->D), "particle replay buffer shape does not match");
     TD3_ARG(r->size > 0 || inject_idx, "train on an empty replay buffer");
     TD3_ARG(r->device == h->cfg.device, "replay buffer lives on another device");
     if (h->stream != s) TD3_HIP(hipStreamSynchronize(h->stream));
@@ -3110,6 +3116,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   *n_stages = n;
   h->last_body = &st;
   h->last_ring = r;
+  h->last_ring_gen = r->gen;
   // the profiled step is a real step: keep the host mirror in sync
   h->total_it += 1;
   h->critic_step += 1;
@@ -3168,7 +3175,8 @@ int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean) {
   TD3_ARG(h->last_body != nullptr, "run td3_profile_stages first");
   TD3_ARG(stage >= 0 && stage <= (int)h->last_body->size(), "stage index out of range");
   TD3_ARG(iters > 0, "iters must be positive");
-  TD3_ARG(stage > 0 || h->last_ring, "stage 0 (the gather) needs the ring of td3_profile_stages");
+  TD3_ARG(stage > 0 || ring_alive(h->last_ring, h->last_ring_gen),
+          "stage 0 (the gather) needs the ring of td3_profile_stages, which was destroyed or replaced");
   TD3_HIP(hipSetDevice(h->cfg.device));
   // stage 0: the stand-alone gather (Philox draw + record reads + batch writes, gather_kernel) of
   // the profiled ring -- a separate launch when the step samples it (Plan::fuse_gather false), the

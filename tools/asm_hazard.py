@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Check the gfx950 ISA of the kernels for the one hand-placed asynchronous load pattern.
+"""Check the gfx950 ISA of the kernels for hand-placed asynchronous loads into registers.
 
-`row_policy_head` (kernels.hip) issues the step-counter load as inline asm with a VGPR output and
-waits for it (`s_waitcnt vmcnt(0)`) only where the Philox noise is drawn.  The compiler treats the
+Round 3's `row_policy_head` (kernels.hip) issued the step-counter load as inline asm with a VGPR
+output and waited for it (`s_waitcnt vmcnt(0)`) only where the Philox noise is drawn (round 4: an
+ordinary divergent load the compiler tracks; `asm_vgpr_loads` must find none).  The compiler treats the
 asm output as defined at the asm statement, so it is free to copy or spill that register before the
 wait; the copy then reads a value that has not landed, and the late load overwrites whatever the
 register was reused for (a round-3 experiment with 256-VGPR heads faulted on Humanoid this way).
@@ -19,6 +20,25 @@ import sys
 _RANGE = re.compile(r"\bv\[(\d+):(\d+)\]")
 _SINGLE = re.compile(r"\bv(\d+)\b")
 _LOAD = re.compile(r"global_load_dword\w*\s+(v\[\d+:\d+\]|v\d+)")
+# a load with a register destination (the LDS-DMA forms, global_load_lds_*, write LDS only)
+_VGPR_LOAD = re.compile(r"\b(global|buffer|flat)_load_(?!lds)\w+\s+(v\[\d+:\d+\]|v\d+)")
+
+
+def asm_vgpr_loads(asm: str) -> list[str]:
+    """Loads into registers issued from inline asm (the compiler cannot track their waits)."""
+    out, func, in_asm = [], "?", False
+    for i, line in enumerate(asm.split("\n")):
+        s = line.strip()
+        m = re.match(r"^(_Z\S+):", s)
+        if m:
+            func = m.group(1)
+        if s.startswith(";;#ASMSTART"):
+            in_asm = True
+        elif s.startswith(";;#ASMEND"):
+            in_asm = False
+        elif in_asm and _VGPR_LOAD.search(s.split(";")[0]):
+            out.append(f"{func}: line {i + 1}: {s}")
+    return out
 
 
 def _regs(text: str) -> set[int]:
@@ -72,7 +92,8 @@ def main(argv):
         print(__doc__)
         return 2
     with open(argv[1]) as f:
-        probs = scan(f.read())
+        text = f.read()
+    probs = scan(text) + asm_vgpr_loads(text)
     for p in probs:
         print(p)
     return 1 if probs else 0
