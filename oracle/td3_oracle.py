@@ -334,19 +334,28 @@ def featured_train_step(L: Learner, batch, noise, record=None, grad_hook=None):
     rec["critic_grads"] = grads
     L.adam_critic(hook(grads))                                                 # :151-153
     if L.total_it % L.policy_freq == 0:                                        # :156
-        pi, (alin, aln, acache, t) = featured_actor(L.actor, L.norm, L.max_action, s)
-        aq1, (qlin, qln, qcache) = featured_q(L.critic, "q1", L.norm, s, pi)   # :159
-        rec.update(pi=pi, actor_q1=aq1, actor_loss=-float(np.mean(aq1, dtype=np.float64)))
-        gq = np.full((B, 1), -1.0 / B, dtype=f32)
-        _, gx = mlp_backward(qlin, qln, qcache, gq)
-        gpi = gx[:, s.shape[1]:]
-        gz = (gpi * f32(L.max_action)) * (f32(1) - t * t)                       # tanh'
-        ag, _ = mlp_backward(alin, aln, acache, gz.astype(f32))
-        agrads = pack_mlp_grads("", ag, L.norm, P=L.actor)
-        rec["actor_grads"] = agrads
+        agrads = featured_actor_grads(L, s, rec)
         L.adam_actor(hook(agrads))                                             # :162-164
         L.polyak()                                                             # :167-171
     return rec
+
+
+def featured_actor_grads(L: Learner, s, record=None):
+    """The actor loss ``-Q1(s, pi(s)).mean()`` and its gradient over the actor's parameters
+    (TD3_featured.py:159-161), with the critic as ``L.critic`` holds it (after the critic step)."""
+    rec = record if record is not None else {}
+    B = s.shape[0]
+    pi, (alin, aln, acache, t) = featured_actor(L.actor, L.norm, L.max_action, s)
+    aq1, (qlin, qln, qcache) = featured_q(L.critic, "q1", L.norm, s, pi)       # :159
+    rec.update(pi=pi, actor_q1=aq1, actor_loss=-float(np.mean(aq1, dtype=np.float64)))
+    gq = np.full((B, 1), -1.0 / B, dtype=f32)
+    _, gx = mlp_backward(qlin, qln, qcache, gq)
+    gpi = gx[:, s.shape[1]:]
+    gz = (gpi * f32(L.max_action)) * (f32(1) - t * t)                           # tanh'
+    ag, _ = mlp_backward(alin, aln, acache, gz.astype(f32))
+    agrads = pack_mlp_grads("", ag, L.norm, P=L.actor)
+    rec["actor_grads"] = agrads
+    return agrads
 
 
 # --------------------------------------------------------------------------- particle path

@@ -16,6 +16,12 @@ added at step t is samplable at step t exactly as in the reference (main.py:261
 before :269).
 ``sample`` draws indices with a device Philox stream instead of the global numpy
 MT19937 (``np.random.randint`` at :120) -- a documented, deliberate difference.
+
+``host_shadow=True`` also keeps the reference's own float64 host arrays (:79-85 / :15-22) of
+every row ``add`` / ``add_batch`` / ``load`` received, written by the same numpy row
+assignments; ``save`` then writes those, so a reference folder loaded and saved back, or a
+run resumed from a build-saved folder, sees the bytes the reference wrote.  Without it ``save``
+writes the fp32 ring (float64(float32(x))).  The fp32 ring stays the training copy either way.
 """
 from __future__ import annotations
 
@@ -86,6 +92,46 @@ class _TorchOrder:
         return False
 
 
+class _HostShadow:
+    """The reference's float64 arrays (``store_np`` order, the reference's shapes), written row
+    by row in ring order with the reference's own assignments (my_replay_buffer.py:109-117)."""
+
+    def __init__(self, arrays, ptr=0):
+        self.arrays = arrays                       # name -> ndarray, first dim = capacity
+        self.cap = next(iter(arrays.values())).shape[0]
+        self.ptr = int(ptr) % self.cap
+        self.valid = True                          # False once a device-only write happened
+
+    @classmethod
+    def zeros(cls, shapes):
+        return cls({k: np.zeros(shp) for k, shp in shapes.items()})
+
+    def put(self, values):
+        """One transition: ``values`` in store_np order (not_done already 1 - done)."""
+        for arr, v in zip(self.arrays.values(), values):
+            arr[self.ptr] = v
+        self.ptr = (self.ptr + 1) % self.cap
+
+    def put_batch(self, values, n):
+        """n transitions (arrays of n rows each), as n consecutive ``put``."""
+        skip = max(0, n - self.cap)                # rows a later row of the batch overwrites
+        rows = (self.ptr + skip + np.arange(n - skip)) % self.cap
+        for arr, v in zip(self.arrays.values(), values):
+            arr[rows] = np.asarray(v).reshape((n,) + arr.shape[1:])[skip:]
+        self.ptr = (self.ptr + n) % self.cap
+
+
+def _save_folder(folder, ptr, size, arrays):
+    """my_replay_buffer.py:91-99 / :24-32: ptr / size pickled (protocol 4), arrays np.save'd."""
+    os.makedirs(folder, exist_ok=True)
+    for attrib, v in (("ptr", int(ptr)), ("size", int(size))):
+        with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
+            pickle.dump(v, f, protocol=4)
+    for attrib, arr in arrays.items():
+        with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
+            np.save(f, arr)
+
+
 def _load_int(path):
     with open(path, "rb") as f:
         v = _SafeIntUnpickler(f).load()
@@ -101,8 +147,10 @@ class ReplayBuffer_featured(object):
     store_pkl = ["ptr", "size"]
 
     def __init__(self, obs_space, action_space, max_size=int(1e6), load_folder=None,
-                 device=None, seed=0):
+                 device=None, seed=0, host_shadow=False):
         self._lib = _lib.load()
+        self.host_shadow = bool(host_shadow)
+        self._shadow = None
         self.state_dim = int(obs_space.shape[0])
         self.action_dim = int(action_space.shape[0])
         self._dev = default_device_index() if device is None else int(device)
@@ -134,6 +182,12 @@ class ReplayBuffer_featured(object):
         # replay.h record: [ s | a | s' | r | not_done | pad ]
         self._cols = (slice(0, sd), slice(sd, sd + ad), slice(sd + ad, 2 * sd + ad),
                       slice(2 * sd + ad, 2 * sd + ad + 1), slice(2 * sd + ad + 1, 2 * sd + ad + 2))
+        self._shadow = _HostShadow.zeros(self._shapes(max_size)) if self.host_shadow else None
+
+    def _shapes(self, n):
+        sd, ad = self.state_dim, self.action_dim
+        return {"state": (n, sd), "action": (n, ad), "next_state": (n, sd), "reward": (n, 1),
+                "not_done": (n, 1)}
 
     def _info(self):
         info = _lib.rb_info_t()
@@ -171,6 +225,8 @@ class ReplayBuffer_featured(object):
         row[cs2] = next_state
         row[cr] = reward
         row[cnd] = 1. - np.asarray(done, dtype=np.float64)
+        if self._shadow is not None:
+            self._shadow.put((state, action, next_state, reward, 1. - done))
         self._n += 1
         if self._n == len(self._stage):
             self.flush()
@@ -184,6 +240,8 @@ class ReplayBuffer_featured(object):
         s2 = np.ascontiguousarray(next_state, dtype=np.float64).reshape(n, self.state_dim)
         r = np.ascontiguousarray(reward, dtype=np.float64).reshape(n)
         d = np.ascontiguousarray(done, dtype=np.float64).reshape(n)
+        if self._shadow is not None:
+            self._shadow.put_batch((s, a, s2, r, 1. - d), n)
         check(self._lib.rb_add(self._h, _lib.dptr(s), _lib.dptr(a), _lib.dptr(s2), _lib.dptr(r),
                                _lib.dptr(d), n, self._stream()), "rb_add")
 
@@ -193,6 +251,8 @@ class ReplayBuffer_featured(object):
     def fill_synthetic(self, n, max_action=1.0, seed=0):
         """Device-side prefill with the SURVEY §8(d) synthetic distribution (bench/tests)."""
         self.flush()
+        if self._shadow is not None:
+            self._shadow.valid = False           # rows the host never saw: save() writes the ring
         check(self._lib.rb_fill_synthetic(self._h, int(n), float(max_action), int(seed),
                                           self._stream()), "rb_fill_synthetic")
 
@@ -242,17 +302,19 @@ class ReplayBuffer_featured(object):
             "not_done": rec[:, 2 * sd + ad + 1:2 * sd + ad + 2].astype(np.float64),
         }
 
+    def _saved_arrays(self, info):
+        sh = self._shadow
+        if sh is not None and sh.valid:
+            assert sh.ptr == int(info.ptr) % sh.cap, "host shadow out of step with the ring"
+            return sh.arrays
+        return self._arrays()
+
     def save(self, folder):
-        """my_replay_buffer.py:91-99: ptr/size pickled (protocol 4), arrays via np.save."""
+        """my_replay_buffer.py:91-99: ptr/size pickled (protocol 4), arrays via np.save (the float64
+        host shadow when kept, else the fp32 ring widened)."""
         self.flush()
-        os.makedirs(folder, exist_ok=True)
         info = self._info()
-        for attrib, v in (("ptr", int(info.ptr)), ("size", int(info.size))):
-            with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
-                pickle.dump(v, f, protocol=4)
-        for attrib, arr in self._arrays().items():
-            with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
-                np.save(f, arr)
+        _save_folder(folder, info.ptr, info.size, self._saved_arrays(info))
 
     def load(self, folder):
         """my_replay_buffer.py:101-107 (pickles are read by an int-only unpickler)."""
@@ -267,6 +329,8 @@ class ReplayBuffer_featured(object):
         self.state_dim = arrs["state"].shape[1]
         self.action_dim = arrs["action"].shape[1]
         self._create(n)
+        if self.host_shadow:                     # the loaded arrays themselves, bytes untouched
+            self._shadow = _HostShadow(arrs, ptr)
         sd, ad = self.state_dim, self.action_dim
         rec = np.zeros((n, self.record_floats), dtype=np.float32)
         rec[:, :sd] = arrs["state"]
@@ -300,8 +364,10 @@ class ReplayBuffer_particles(object):
     store_pkl = ["ptr", "size"]
 
     def __init__(self, obs_space, action_space, max_size=int(1e6), load_folder=None,
-                 device=None, seed=0):
+                 device=None, seed=0, host_shadow=False):
         self._lib = _lib.load()
+        self.host_shadow = bool(host_shadow)
+        self._shadow = None
         self.feat_dim = int(obs_space[0].shape[0])
         self.n_particles, self.particle_dim = (int(x) for x in obs_space[1].shape)
         self.action_dim = int(action_space.shape[0])
@@ -330,6 +396,13 @@ class ReplayBuffer_particles(object):
         self.record_floats = self._info().record_floats
         _new_stage(self, max(1, _STAGE_ROWS // 16))
         self._cols = tuple(slice(c, c + w) for c, w in self._offsets().values())
+        self._shadow = _HostShadow.zeros(self._shapes(max_size)) if self.host_shadow else None
+
+    def _shapes(self, n):
+        F, A, nd = self.feat_dim, self.action_dim, (self.n_particles, self.particle_dim)
+        return {"state_features": (n, F), "state_particles": (n, *nd), "action": (n, A),
+                "next_state_features": (n, F), "next_state_particles": (n, *nd), "reward": (n, 1),
+                "not_done": (n, 1)}
 
     def _info(self):
         info = _lib.rb_info_t()
@@ -372,6 +445,8 @@ class ReplayBuffer_particles(object):
         row[cp2].reshape(nd)[...] = next_state[1]
         row[cr] = reward
         row[cnd] = 1. - np.asarray(done, dtype=np.float64)
+        if self._shadow is not None:
+            self._shadow.put((state[0], state[1], action, next_state[0], next_state[1], reward, 1. - done))
         self._n += 1
         if self._n == len(self._stage):
             self.flush()
@@ -387,6 +462,8 @@ class ReplayBuffer_particles(object):
                 np.ascontiguousarray(next_part, dtype=np.float64).reshape(n, npd),
                 np.ascontiguousarray(reward, dtype=np.float64).reshape(n),
                 np.ascontiguousarray(done, dtype=np.float64).reshape(n)]
+        if self._shadow is not None:
+            self._shadow.put_batch(arrs[:6] + [1. - arrs[6]], n)
         check(self._lib.rb_add_particles(self._h, *[_lib.dptr(x) for x in arrs], n, self._stream()),
               "rb_add_particles")
 
@@ -395,6 +472,8 @@ class ReplayBuffer_particles(object):
 
     def fill_synthetic(self, n, max_action=1.0, seed=0):
         self.flush()
+        if self._shadow is not None:
+            self._shadow.valid = False
         check(self._lib.rb_fill_synthetic(self._h, int(n), float(max_action), int(seed), self._stream()),
               "rb_fill_synthetic")
 
@@ -439,22 +518,22 @@ class ReplayBuffer_particles(object):
         return o
 
     def save(self, folder):
-        """my_replay_buffer.py:24-32 (ptr / size pickled with protocol 4, arrays np.save'd)."""
+        """my_replay_buffer.py:24-32 (ptr / size pickled with protocol 4, arrays np.save'd; the
+        float64 host shadow when kept)."""
         self.flush()
-        os.makedirs(folder, exist_ok=True)
         info = self._info()
-        for attrib, v in (("ptr", int(info.ptr)), ("size", int(info.size))):
-            with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
-                pickle.dump(v, f, protocol=4)
+        sh = self._shadow
+        if sh is not None and sh.valid:
+            assert sh.ptr == int(info.ptr) % sh.cap, "host shadow out of step with the ring"
+            _save_folder(folder, info.ptr, info.size, sh.arrays)
+            return
         n = self.max_size
         rec = np.empty((n, self.record_floats), dtype=np.float32)
         check(self._lib.rb_read_records(self._h, 0, n, _lib.fptr(rec)), "rb_read_records")
-        shapes = {"state_particles": (n, self.n_particles, self.particle_dim),
-                  "next_state_particles": (n, self.n_particles, self.particle_dim)}
-        for name, (c, w) in self._offsets().items():
-            arr = rec[:, c:c + w].astype(np.float64).reshape(shapes.get(name, (n, w)))
-            with open(os.path.join(folder, name + ".pkl"), "wb") as f:
-                np.save(f, arr)
+        shapes = self._shapes(n)
+        _save_folder(folder, info.ptr, info.size,
+                     {name: rec[:, c:c + w].astype(np.float64).reshape(shapes[name])
+                      for name, (c, w) in self._offsets().items()})
 
     def load(self, folder):
         """my_replay_buffer.py:34-44 (int-only unpickler for ptr / size)."""
@@ -470,6 +549,8 @@ class ReplayBuffer_particles(object):
         self.n_particles, self.particle_dim = arrs["state_particles"].shape[1:3]
         self.action_dim = arrs["action"].shape[1]
         self._create(n)
+        if self.host_shadow:
+            self._shadow = _HostShadow(arrs, ptr)
         rec = np.zeros((n, self.record_floats), dtype=np.float32)
         for name, (c, w) in self._offsets().items():
             rec[:, c:c + w] = arrs[name].reshape(n, w)

@@ -147,3 +147,102 @@ def test_replay_buffer_files_roundtrip(tmp_path):
     idx = np.arange(cap)
     for x, y in zip(rb.sample(cap, indices=idx), rb2.sample(cap, indices=idx)):
         np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+
+
+def _reference_save(folder, buf, names):
+    """The reference's ``save`` (my_replay_buffer.py:91-99) over an oracle buffer's arrays."""
+    os.makedirs(folder, exist_ok=True)
+    for attrib in ("ptr", "size"):
+        with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
+            pickle.dump(getattr(buf, attrib), f, protocol=4)
+    for attrib in names:
+        with open(os.path.join(folder, attrib + ".pkl"), "wb") as f:
+            np.save(f, getattr(buf, attrib))
+
+
+def _same_files(a, b, names):
+    for n in ("ptr", "size", *names):
+        with open(os.path.join(a, n + ".pkl"), "rb") as fa, open(os.path.join(b, n + ".pkl"), "rb") as fb:
+            assert fa.read() == fb.read(), n
+
+
+FEAT = ["state", "action", "next_state", "reward", "not_done"]
+PART = ["state_features", "state_particles", "action", "next_state_features", "next_state_particles",
+        "reward", "not_done"]
+
+
+def test_reference_buffer_folder_roundtrips_byte_exact(tmp_path):
+    """host_shadow=True: a folder in the reference's format (float64 values an fp32 ring cannot
+    hold) loads and saves back byte for byte, and rows added after the load are saved as the
+    reference's own add would have stored them (my_replay_buffer.py:101-117)."""
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+    from test_gpu_parity import Box
+    sd, ad, cap = 5, 2, 64
+    rs = np.random.RandomState(4)
+    ref = orc.FeaturedBuffer(sd, ad, cap)
+    for _ in range(40):
+        ref.add(rs.standard_normal(sd), rs.uniform(-1, 1, ad), rs.standard_normal(sd), rs.standard_normal(),
+                float(rs.uniform() < 0.2))
+    _reference_save(tmp_path / "ref", ref, FEAT)
+    rb = ReplayBuffer_featured(Box((sd,)), Box((ad,)), load_folder=str(tmp_path / "ref"), host_shadow=True)
+    rb.save(str(tmp_path / "out"))
+    _same_files(tmp_path / "ref", tmp_path / "out", FEAT)
+    # continue both: single adds and one bulk add that wraps the ring
+    for _ in range(10):
+        t = (rs.standard_normal(sd), rs.uniform(-1, 1, ad), rs.standard_normal(sd), rs.standard_normal(),
+             float(rs.uniform() < 0.2))
+        ref.add(*t)
+        rb.add(*t)
+    n = 30
+    bulk = (rs.standard_normal((n, sd)), rs.uniform(-1, 1, (n, ad)), rs.standard_normal((n, sd)),
+            rs.standard_normal(n), (rs.uniform(size=n) < 0.2).astype(np.float64))
+    for i in range(n):
+        ref.add(*(x[i] for x in bulk))
+    rb.add_batch(*bulk)
+    _reference_save(tmp_path / "ref2", ref, FEAT)
+    rb.save(str(tmp_path / "out2"))
+    _same_files(tmp_path / "ref2", tmp_path / "out2", FEAT)
+    # the training copy is the fp32 ring of the same rows
+    idx = np.arange(cap)
+    for x, y in zip(rb.sample(cap, indices=idx), ref.gather(idx)):
+        np.testing.assert_array_equal(x.cpu().numpy(), y)
+
+
+def test_reference_particle_buffer_folder_roundtrips_byte_exact(tmp_path):
+    from td3_amd.my_replay_buffer import ReplayBuffer_particles
+    from test_gpu_parity import Box
+    F, N, D, A, cap = 7, 16, 9, 3, 24
+    rs = np.random.RandomState(6)
+    ref = orc.ParticleBuffer(F, N, D, A, cap)
+
+    def trans():
+        return ((rs.standard_normal(F), rs.standard_normal((N, D))), rs.uniform(-1, 1, A),
+                (rs.standard_normal(F), rs.standard_normal((N, D))), rs.standard_normal(),
+                float(rs.uniform() < 0.2))
+    for _ in range(30):                                 # wraps
+        ref.add(*trans())
+    _reference_save(tmp_path / "ref", ref, PART)
+    obs = (Box((F,)), Box((N, D)))
+    rb = ReplayBuffer_particles(obs, Box((A,)), load_folder=str(tmp_path / "ref"), host_shadow=True)
+    rb.save(str(tmp_path / "out"))
+    _same_files(tmp_path / "ref", tmp_path / "out", PART)
+    for _ in range(5):
+        t = trans()
+        ref.add(*t)
+        rb.add(*t)
+    _reference_save(tmp_path / "ref2", ref, PART)
+    rb.save(str(tmp_path / "out2"))
+    _same_files(tmp_path / "ref2", tmp_path / "out2", PART)
+
+
+def test_buffer_without_shadow_after_synthetic_fill_saves_the_ring(tmp_path):
+    """A device-only write (fill_synthetic) invalidates the shadow: save falls back to the ring."""
+    from td3_amd.my_replay_buffer import ReplayBuffer_featured
+    from test_gpu_parity import Box
+    rb = ReplayBuffer_featured(Box((3,)), Box((1,)), max_size=32, host_shadow=True)
+    rb.fill_synthetic(32, 2.0, seed=3)
+    rb.save(str(tmp_path))
+    with open(tmp_path / "state.pkl", "rb") as f:
+        st = np.load(f)
+    assert st.dtype == np.float64 and np.abs(st).max() > 0
+    np.testing.assert_array_equal(st, st.astype(np.float32).astype(np.float64))
