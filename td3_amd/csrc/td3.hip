@@ -197,8 +197,17 @@ struct LocalGroup {
   std::vector<td3_handle*> hs;
 };
 
+// The split-K dW stages' partial slab: one per plan, sized to its largest stage.  A plan's stages run
+// one after another on one stream (and a stage's combine consumes the slab right behind it), so every
+// split-K stage of the plan can share it (launch_dw_split reads the pointer at launch).
+struct SlabRef {
+  float* p = nullptr;
+  size_t bytes = 0;
+};
+
 struct Plan {
   int B = 0, Bp = 0;
+  SlabRef dwslab;
   float* scratch = nullptr;
   size_t scratch_bytes = 0;
   // inputs
@@ -844,7 +853,7 @@ static int dwsk_matrix_weight() { return std::max(1, env_int("TD3_DWSK_WM", 6));
 static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                         Group& g, int which, const std::vector<BwdItem>& items, int Bp,
                         const char* tag, bool polyak, int enc_nwg = 0,
-                        const std::vector<const float*>* unit_scale = nullptr) {
+                        const std::vector<const float*>* unit_scale = nullptr, SlabRef* slab = nullptr) {
   const bool norm = h->cfg.norm == 1;
   // B >= 512: 64x64 weight tiles with LDS-staged operands (dw64_kernel: half the operand
   // traffic, Humanoid C_dw 73 -> 63 us), else 32x32 register tiles (dw_kernel: more, shorter
@@ -993,11 +1002,15 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     TD3_RC(upload(h, owned, idx.data(), idx.size() * sizeof(int), &d));
     k.wg_unit = static_cast<const int*>(d);
     k.tile_wg = k.wg_unit + k.G + 1;
-    void* slab = nullptr;
-    TD3_HIP(hipMalloc(&slab, (size_t)k.G * k.J * k.slot * sizeof(float)));
-    owned.push_back(slab);
-    k.slab = static_cast<float*>(slab);
-    st.push_back({std::string(tag) + "_dw", [=](hipStream_t s) { return launch_dw_split(a, k, s); }, flops,
+    TD3_ARG(slab != nullptr, "internal: split-K dW stage without a plan slab");
+    slab->bytes = std::max(slab->bytes, (size_t)k.G * k.J * k.slot * sizeof(float));
+    st.push_back({std::string(tag) + "_dw",
+                  [=](hipStream_t s) {
+                    DwSplit kk = k;
+                    kk.slab = slab->p;
+                    return launch_dw_split(a, kk, s);
+                  },
+                  flops,
                   std::string("td3::dwsk_kernel<") + (unit_scale ? "true, " : "false, ") +
                       (tm == 128 ? "true>" : "false>")});
   } else {
@@ -1056,6 +1069,15 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                   [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s); }, 0,
                   "td3::adam_flat_kernel"});
   }
+  return 0;
+}
+
+static int alloc_dw_slab(Plan* P) {
+  if (!P->dwslab.bytes) return 0;
+  void* d = nullptr;
+  TD3_HIP(hipMalloc(&d, P->dwslab.bytes));
+  P->tables.push_back(d);
+  P->dwslab.p = static_cast<float*>(d);
   return 0;
 }
 
@@ -1294,7 +1316,7 @@ static int build_step(td3_handle* h, int B) {
         }
         TD3_RC(push_row2_stage(st, rows, kRowTargetLoss, kRowLnBwd, 1, Bp, "critic_loss"));
         const std::vector<const float*> usc = {P->gscale[0], P->gscale[1]};
-        TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, 0, &usc));
+        TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, 0, &usc, &P->dwslab));
       } else {
         // ---- heads: a' = target smoothing into X_S2A (:131-137); pi(s) into X_SP (:159)
         {
@@ -1350,7 +1372,7 @@ static int build_step(td3_handle* h, int B) {
         }
         std::vector<BwdItem> cb = {{&q1, Pq1, &P->Q[0], true}, {&q2, Pq2, &P->Q[1], true}};
         TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true));
-        TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0));
+        TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, 0, nullptr, &P->dwslab));
       }
       if (!actor_phase) continue;
       // ---------------- delayed policy update (TD3_featured.py:156-171)
@@ -1400,7 +1422,7 @@ static int build_step(td3_handle* h, int B) {
       }
       std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
       TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true));
-      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true));
+      TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, 0, nullptr, &P->dwslab));
     }
   }
   for (int a = 0; a < 2; ++a)          // ring bodies: F_fwd0 sampled from the ring, the rest shared
@@ -1408,6 +1430,7 @@ static int build_step(td3_handle* h, int B) {
       std::vector<Stage>& br = P->body_ring[a][i];
       br.insert(br.end(), P->body[a][i].begin() + 1, P->body[a][i].end());
     }
+  TD3_RC(alloc_dw_slab(P.get()));
   if (h->plan) destroy_plan(h->plan.get());
   h->plan = std::move(P);
   return 0;
@@ -1690,7 +1713,7 @@ static int build_step_particles(td3_handle* h, int B) {
     std::vector<BwdItem> ab = {{&an, Pa, &P->A, true}};
     TD3_RC(add_bwd_stages(h, P->tables, st, ab, Bp, B, "AB", true, true));
     push_enc_bwd(h, Pp, st, ab, {P->XA}, "AB_enc");
-    TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, P->nwg_a));
+    TD3_RC(add_dw_stage(h, P->tables, st, h->actor, 1, ab, Bp, "A", true, P->nwg_a, nullptr, &P->dwslab));
     return 0;
   };
 
@@ -1777,7 +1800,7 @@ static int build_step_particles(td3_handle* h, int B) {
       }
       TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true, true));
       push_enc_bwd(h, Pp, st, cb, cbx, "CB_enc");
-      TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, P->nwg));
+      TD3_RC(add_dw_stage(h, P->tables, st, h->critic, 0, cb, Bp, "C", actor_phase != 0, P->nwg, nullptr, &P->dwslab));
       if (!actor_phase) continue;
       TD3_RC(actor_phase_stages(st));
     }
@@ -1799,6 +1822,7 @@ static int build_step_particles(td3_handle* h, int B) {
     st.push_back({"L_polyak_critic", [=](hipStream_t s) { return launch_polyak_flat(Tc, Pc, nc, tau, s); }, 0,
                   "td3::polyak_flat_kernel"});
   }
+  TD3_RC(alloc_dw_slab(P.get()));
   if (h->plan) destroy_plan(h->plan.get());
   h->plan = std::move(P);
   return 0;
