@@ -87,8 +87,8 @@ def stage_table(pol, rb, batch, iters=50, reps=5):
         kernels = [lib.td3_stage_kernel(h, i).decode() for i in range(n.value)]
         flops = [lib.td3_stage_flops(h, i) for i in range(n.value)]
         for i in range(1, n.value):
-            if names[i].endswith("_allreduce"):
-                continue          # a collective cannot be re-launched on its own
+            if names[i].endswith("_allreduce") or names[i].endswith("_join"):
+                continue          # a collective (or the comm-stream join) cannot be re-launched on its own
             t = C.c_float()
             runs = []
             for _ in range(reps):

@@ -188,6 +188,11 @@ struct Stage {
   std::string kernel;   // HIP kernel function the stage launches (rocprof name)
   std::shared_ptr<GemmLaunch> gemm;   // GEMM stages only
   int collective = -1;  // data parallel: the gradient all-reduce of group 0 (actor) / 1 (critic)
+  // the all-reduced range of the group's G arena (floats; coll_n < 0: the whole arena) and, for a
+  // bucket of the overlapped schedule, the optimizer step of that range the in-process seam runs
+  // on its own stream after the fixed-order sum (RCCL mode: both queued on the comm stream)
+  int64_t coll_off = 0, coll_n = -1;
+  std::function<int(hipStream_t)> after;
 };
 
 // Replicas of one process sharing a device (td3_comm_init_local): the test seam of the data-parallel
@@ -208,6 +213,7 @@ struct SlabRef {
 struct Plan {
   int B = 0, Bp = 0;
   SlabRef dwslab;
+  bool dp_overlap = false;              // stages queue work on the comm stream: launched directly
   float* scratch = nullptr;
   size_t scratch_bytes = 0;
   // inputs
@@ -341,6 +347,11 @@ struct td3_handle {
   std::unique_ptr<Plan> plan;
   std::map<int, std::unique_ptr<ActPlan>> act;
   ncclComm_t comm = nullptr;
+  // the overlapped data-parallel schedule (add_dw_stage buckets): the all-reduces and the per-bucket
+  // optimizer steps run on comm_stream, ordered after the bucket's dW by comm_ev (recorded on the step
+  // stream) and joined back by comm_done before the next stage that reads the parameters
+  hipStream_t comm_stream = nullptr;
+  hipEvent_t comm_ev = nullptr, comm_done = nullptr;
   std::shared_ptr<LocalGroup> local;          // td3_comm_init_local (comm stays null)
   int nranks = 1, rank = 0;
   std::vector<Stage>* last_body = nullptr;
@@ -846,6 +857,83 @@ constexpr int kDwSplitWorkgroups = TD3_DWSK_G;   // one per CU of the MI355X
 static int dwsk_tile_edge() { return env_int("TD3_DWSK_T", 64) == 128 ? 128 : 64; }
 static int dwsk_matrix_weight() { return std::max(1, env_int("TD3_DWSK_WM", 6)); }
 
+// The overlapped (bucketed) data-parallel dW schedule: TD3_DP_BUCKETS = 0 off; 1 (default) for real
+// peers (RCCL, nranks > 1) and the in-process seam; 2 also on a one-rank communicator (bench.py
+// --dp-self: the schedule's price without peers).  Read when a plan is built.
+static bool dp_overlap(const td3_handle* h) {
+  const int m = env_int("TD3_DP_BUCKETS", 1);
+  if (m <= 0) return false;
+  if (h->local) return true;
+  return h->comm && (h->nranks > 1 || m >= 2);
+}
+
+// The split-K partition of a dW stage's problems (kernels.h DwSplit): every tile's 64-row steps in
+// one weighted list, cut evenly over one workgroup per CU; per problem its tm x tm matrix tiles (n tile
+// major, so an XCD's consecutive tiles share dZ column blocks), then its 32-column vector tiles.  The
+// tile list and the partition are uploaded into `owned`; the partial slab is the plan's (`slab`).
+static int make_dw_split(td3_handle* h, std::vector<void*>& owned, const DwArgs& a, SlabRef* slab, DwSplit& out) {
+  const int tm = dwsk_tile_edge();
+  const int wm = dwsk_matrix_weight();
+  std::vector<DwTile> tiles;
+  std::vector<int> wt;                          // cost of one 64-row step of the tile
+  for (int pi = 0; pi < a.nprob; ++pi) {
+    const DwProb& p = a.probs[pi];
+    if (p.ntk > 0) {
+      for (int nt = 0; nt < (p.Np + tm - 1) / tm; ++nt)
+        for (int kt = 0; kt < (p.Kp + tm - 1) / tm; ++kt) {
+          tiles.push_back(DwTile{pi, 0, nt, kt});
+          // MFMA work of the busiest SIMD (dwsk_matrix128's quadrant map), out of 4 quadrants
+          const int an = std::min(tm, p.Np - nt * tm) / 32, ak = std::min(tm, p.Kp - kt * tm) / 32;
+          const int q = tm == 128 ? (an > 2 ? 2 : 1) * (ak > 2 ? 2 : 1) : 1;
+          wt.push_back(2 + wm * q / 4);
+        }
+    }
+    for (int j = 0; j < p.Np / 32; ++j) {
+      tiles.push_back(DwTile{pi, 1, j, 0});
+      wt.push_back(1);
+    }
+  }
+  DwSplit k{};
+  k.ntile = (int)tiles.size();
+  k.S = a.Bp / 64;
+  k.G = kDwSplitWorkgroups;
+  k.tm = tm;
+  k.slot = tm * tm;
+  const int units = k.ntile * k.S;
+  int64_t wtot = 0;
+  for (int w : wt) wtot += (int64_t)w * k.S;
+  const int64_t cw = (wtot + k.G - 1) / k.G;
+  // unit -> workgroup by the unit's weighted midpoint: nondecreasing, every workgroup ~cw of cost
+  std::vector<int> idx(k.G + 1 + 2 * k.ntile, units);   // [wg_unit (G + 1)][tile_wg (2 ntile)]
+  std::vector<int> vu(units);
+  int64_t pos = 0;
+  int vcur = 0;
+  idx[0] = 0;
+  for (int u = 0; u < units; ++u) {
+    const int w = wt[u / k.S];
+    const int v = (int)std::min<int64_t>(k.G - 1, (2 * pos + w) / (2 * cw));
+    while (vcur < v) idx[++vcur] = u;
+    vu[u] = v;
+    pos += w;
+  }
+  for (int t = 0; t < k.ntile; ++t) {
+    idx[k.G + 1 + 2 * t] = vu[t * k.S];
+    idx[k.G + 1 + 2 * t + 1] = vu[t * k.S + k.S - 1];
+  }
+  for (int v = 0; v < k.G; ++v)                 // partial slots: the tiles one workgroup's units touch
+    if (idx[v] < idx[v + 1]) k.J = std::max(k.J, (idx[v + 1] - 1) / k.S - idx[v] / k.S + 1);
+  void* d = nullptr;
+  TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
+  k.tiles = static_cast<const DwTile*>(d);
+  TD3_RC(upload(h, owned, idx.data(), idx.size() * sizeof(int), &d));
+  k.wg_unit = static_cast<const int*>(d);
+  k.tile_wg = k.wg_unit + k.G + 1;
+  TD3_ARG(slab != nullptr, "internal: split-K dW stage without a plan slab");
+  slab->bytes = std::max(slab->bytes, (size_t)k.G * k.J * k.slot * sizeof(float));
+  out = k;
+  return 0;
+}
+
 // Weight / bias / LN grads of every layer of `items`, fused with the optimizer.
 // enc (TD3_particles): the encoder partial slabs of `items` (reduced + optimizer in one launch).
 // unit_scale (featured critic): per item, the dense [Bp] row scale g_r of its unit-gradient
@@ -942,68 +1030,91 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.mode = (dp || wn) ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
   a.tile64 = tile64 ? 1 : 0;
   a.scaled = unit_scale ? 1 : 0;
-  if (tile64 && Bp % 64 == 0 && TD3_DWSK) {
-    // split-K persistent path (kernels.h DwSplit): every tile's 64-row steps in one weighted list,
-    // cut evenly over one workgroup per CU; per problem its tm x tm matrix tiles (n tile major, so an
-    // XCD's consecutive tiles share dZ column blocks), then its 32-column vector tiles
-    const int tm = dwsk_tile_edge();
-    const int wm = dwsk_matrix_weight();
-    std::vector<DwTile> tiles;
-    std::vector<int> wt;                          // cost of one 64-row step of the tile
-    for (int pi = 0; pi < a.nprob; ++pi) {
-      const DwProb& p = a.probs[pi];
-      if (p.ntk > 0) {
-        for (int nt = 0; nt < (p.Np + tm - 1) / tm; ++nt)
-          for (int kt = 0; kt < (p.Kp + tm - 1) / tm; ++kt) {
-            tiles.push_back(DwTile{pi, 0, nt, kt});
-            // MFMA work of the busiest SIMD (dwsk_matrix128's quadrant map), out of 4 quadrants
-            const int an = std::min(tm, p.Np - nt * tm) / 32, ak = std::min(tm, p.Kp - kt * tm) / 32;
-            const int q = tm == 128 ? (an > 2 ? 2 : 1) * (ak > 2 ? 2 : 1) : 1;
-            wt.push_back(2 + wm * q / 4);
-          }
+  const int tm = dwsk_tile_edge();
+  const bool split = tile64 && Bp % 64 == 0 && TD3_DWSK;
+  if (dp && split && !wn && enc_nwg == 0 && items.size() >= 2 && dp_overlap(h)) {
+    // The overlapped data-parallel schedule, one bucket per network of the group in
+    // arena order: bucket k's split-K dW (gradient only) on the step stream, then -- on the comm
+    // stream, behind an event -- the all-reduce of the network's arena range and its Adam (+ Polyak),
+    // while the step stream already runs bucket k+1's dW.  One join before the next stage reads the
+    // parameters.  The in-process seam runs the same buckets: a fixed-order sum of the range, then
+    // the bucket's optimizer step (Stage::after), on its one stream.
+    const bool local = h->local != nullptr;
+    ncclComm_t comm = h->comm;
+    hipStream_t cs = h->comm_stream;
+    hipEvent_t ev = h->comm_ev, done = h->comm_done;
+    TD3_ARG(local || (cs && ev && done), "internal: data-parallel handle without a comm stream");
+    const int pol = polyak ? 1 : 0;
+    const std::string kname = std::string("td3::dwsk_kernel<") + (unit_scale ? "true, " : "false, ") +
+                              (tm == 128 ? "true>" : "false>");
+    int p0 = 0;
+    for (size_t b = 0; b < items.size(); ++b) {
+      const NetL& n = *items[b].net;
+      const int cnt = 4 + (n.lnin ? 1 : 0);
+      DwArgs ab = a;
+      ab.nprob = cnt;
+      double fb = 0;
+      for (int i = 0; i < cnt; ++i) {
+        ab.probs[i] = a.probs[p0 + i];
+        if (i < 4) fb += 2.0 * Bp * n.lin[i].N * n.lin[i].K;
       }
-      for (int j = 0; j < p.Np / 32; ++j) {
-        tiles.push_back(DwTile{pi, 1, j, 0});
-        wt.push_back(1);
-      }
+      p0 += cnt;
+      DwSplit kb{};
+      TD3_RC(make_dw_split(h, owned, ab, slab, kb));
+      const std::string bn = std::string(tag) + "_dw_" + std::to_string(b);
+      st.push_back({bn,
+                    [=](hipStream_t s) {
+                      DwSplit kk = kb;
+                      kk.slab = slab->p;
+                      return launch_dw_split(ab, kk, s);
+                    },
+                    fb, kname});
+      const int64_t off = n.enc_off >= 0 ? n.enc_off : n.lin[0].offW;
+      const int64_t end = b + 1 < items.size()
+                              ? (items[b + 1].net->enc_off >= 0 ? items[b + 1].net->enc_off : items[b + 1].net->lin[0].offW)
+                              : g.size;
+      TD3_ARG(off >= 0 && end > off && end <= g.size, "internal: bucket range");
+      const int64_t nb = end - off;
+      AdamArgs ar = a.adam;
+      ar.P += off; ar.G += off; ar.M += off; ar.V += off; ar.T += off;
+      ar.grad_scale = 1.0f / (float)h->nranks;
+      float* Gb = g.G + off;
+      st.push_back({std::string(tag) + "_" + std::to_string(b) + "_allreduce",
+                    [=](hipStream_t s) {
+                      if (local) {
+                        set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
+                        return -1;
+                      }
+                      TD3_HIP(hipEventRecord(ev, s));
+                      TD3_HIP(hipStreamWaitEvent(cs, ev, 0));
+                      ncclResult_t r = ncclAllReduce(Gb, Gb, (size_t)nb, ncclFloat, ncclSum, comm, cs);
+                      if (r != ncclSuccess) {
+                        set_error("ncclAllReduce: %s", ncclGetErrorString(r));
+                        return -2;
+                      }
+                      TD3_RC(launch_adam_flat(ar, nb, pol, cs));
+                      TD3_HIP(hipEventRecord(done, cs));
+                      return 0;
+                    },
+                    0, "rccl"});
+      Stage& cst = st.back();
+      cst.collective = which == 1 ? 0 : 1;
+      cst.coll_off = off;
+      cst.coll_n = nb;
+      cst.after = [=](hipStream_t s) { return launch_adam_flat(ar, nb, pol, s); };
     }
+    st.push_back({std::string(tag) + "_join",
+                  [=](hipStream_t s) {
+                    if (local) return 0;            // the seam ran the buckets on its stream
+                    TD3_HIP(hipStreamWaitEvent(s, done, 0));
+                    return 0;
+                  },
+                  0, "(stream join)"});
+    return 0;
+  }
+  if (split) {
     DwSplit k{};
-    k.ntile = (int)tiles.size();
-    k.S = Bp / 64;
-    k.G = kDwSplitWorkgroups;
-    k.tm = tm;
-    k.slot = tm * tm;
-    const int units = k.ntile * k.S;
-    int64_t wtot = 0;
-    for (int w : wt) wtot += (int64_t)w * k.S;
-    const int64_t cw = (wtot + k.G - 1) / k.G;
-    // unit -> workgroup by the unit's weighted midpoint: nondecreasing, every workgroup ~cw of cost
-    std::vector<int> idx(k.G + 1 + 2 * k.ntile, units);   // [wg_unit (G + 1)][tile_wg (2 ntile)]
-    std::vector<int> vu(units);
-    int64_t pos = 0;
-    int vcur = 0;
-    idx[0] = 0;
-    for (int u = 0; u < units; ++u) {
-      const int w = wt[u / k.S];
-      const int v = (int)std::min<int64_t>(k.G - 1, (2 * pos + w) / (2 * cw));
-      while (vcur < v) idx[++vcur] = u;
-      vu[u] = v;
-      pos += w;
-    }
-    for (int t = 0; t < k.ntile; ++t) {
-      idx[k.G + 1 + 2 * t] = vu[t * k.S];
-      idx[k.G + 1 + 2 * t + 1] = vu[t * k.S + k.S - 1];
-    }
-    for (int v = 0; v < k.G; ++v)                 // partial slots: the tiles one workgroup's units touch
-      if (idx[v] < idx[v + 1]) k.J = std::max(k.J, (idx[v + 1] - 1) / k.S - idx[v] / k.S + 1);
-    void* d = nullptr;
-    TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
-    k.tiles = static_cast<const DwTile*>(d);
-    TD3_RC(upload(h, owned, idx.data(), idx.size() * sizeof(int), &d));
-    k.wg_unit = static_cast<const int*>(d);
-    k.tile_wg = k.wg_unit + k.G + 1;
-    TD3_ARG(slab != nullptr, "internal: split-K dW stage without a plan slab");
-    slab->bytes = std::max(slab->bytes, (size_t)k.G * k.J * k.slot * sizeof(float));
+    TD3_RC(make_dw_split(h, owned, a, slab, k));
     st.push_back({std::string(tag) + "_dw",
                   [=](hipStream_t s) {
                     DwSplit kk = k;
@@ -1431,6 +1542,7 @@ static int build_step(td3_handle* h, int B) {
       br.insert(br.end(), P->body[a][i].begin() + 1, P->body[a][i].end());
     }
   TD3_RC(alloc_dw_slab(P.get()));
+  P->dp_overlap = (h->comm || h->local) && dp_overlap(h);
   if (h->plan) destroy_plan(h->plan.get());
   h->plan = std::move(P);
   return 0;
@@ -1823,6 +1935,7 @@ static int build_step_particles(td3_handle* h, int B) {
                   "td3::polyak_flat_kernel"});
   }
   TD3_RC(alloc_dw_slab(P.get()));
+  P->dp_overlap = (h->comm || h->local) && dp_overlap(h);
   if (h->plan) destroy_plan(h->plan.get());
   h->plan = std::move(P);
   return 0;
@@ -1961,7 +2074,7 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
   // asking the stream queues a marker, a per-step drain) training launches directly.
   // Data parallel (RCCL comm attached): auto launches directly, so every rank issues its
   // all-reduces the same way whatever its local progress (no captured / uncaptured mix).
-  const bool graph = !h->probing && (h->cfg.use_graph == 1 ||
+  const bool graph = !h->probing && !P->dp_overlap && (h->cfg.use_graph == 1 ||
                                       (h->cfg.use_graph == 2 && !h->comm && !actor_phase && h->act_used &&
                                        hipEventQuery(h->actor_ev) != hipErrorNotReady));
   if (!graph) {
@@ -2503,6 +2616,12 @@ int td3_destroy(td3_handle* h) {
     (void)hipFree(kv.second->scratch);
     if (kv.second->hio) (void)hipHostFree(kv.second->hio);
   }
+  if (h->comm_stream) {
+    (void)hipStreamSynchronize(h->comm_stream);
+    (void)hipStreamDestroy(h->comm_stream);
+    (void)hipEventDestroy(h->comm_ev);
+    (void)hipEventDestroy(h->comm_done);
+  }
   if (h->comm) ncclCommDestroy(h->comm);
   if (h->local)       // the group loses a member: the rest refuse td3_train_step_local from now on
     for (auto& m : h->local->hs)
@@ -2983,6 +3102,11 @@ int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int ra
   h->comm = c;
   h->nranks = nranks;
   h->rank = rank;
+  if (!h->comm_stream) {
+    TD3_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
+    TD3_HIP(hipEventCreateWithFlags(&h->comm_ev, hipEventDisableTiming));
+    TD3_HIP(hipEventCreateWithFlags(&h->comm_done, hipEventDisableTiming));
+  }
   if (h->plan) {           // stage lists change (grad write + all-reduce + flat Adam)
     int B = h->plan->B;
     TD3_RC(build_plan(h, B));
@@ -3077,13 +3201,19 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
     if (coll < 0) break;
     LocalSumArgs a{};
     a.n = n;
+    std::vector<const Stage*> cst(n);
     for (int k = 0; k < n; ++k) {
       Group& grp = coll == 0 ? hs[k]->actor : hs[k]->critic;
-      a.a[k] = grp.G;
-      a.size = grp.size;
+      cst[k] = &(*lists[k])[pos[k]];
+      a.a[k] = grp.G + cst[k]->coll_off;
+      a.size = cst[k]->coll_n < 0 ? grp.size : cst[k]->coll_n;
+      TD3_ARG(cst[k]->coll_off == cst[0]->coll_off && cst[k]->coll_n == cst[0]->coll_n,
+              "internal: replicas reached different all-reduce buckets");
       ++pos[k];
     }
     TD3_RC(launch_local_sum(a, s));
+    for (int k = 0; k < n; ++k)               // the bucket's optimizer step behind its sum
+      if (cst[k]->after) TD3_RC(cst[k]->after(s));
   }
   for (int k = 0; k < n; ++k) TD3_RC(ring_end_read(reinterpret_cast<Ring*>(rbs[k]), s));
   if (inject_idx || inject_noise) TD3_HIP(hipStreamSynchronize(s));

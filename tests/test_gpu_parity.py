@@ -347,6 +347,43 @@ def test_allreduce_path_single_rank(name):
         _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"))
 
 
+def test_overlapped_allreduce_schedule_single_rank(monkeypatch):
+    """The overlapped data-parallel schedule (td3.hip add_dw_stage buckets: per-network split-K dW,
+    then the all-reduce of the network's arena range and its Adam on the comm stream, joined back
+    before the next stage) through RCCL at nranks = 1 (TD3_DP_BUCKETS=2 turns it on without peers):
+    Humanoid widths at B = 1024, a critic-only and a policy step against the oracle, both Adam moments
+    included."""
+    import ctypes as C
+    from td3_amd import _lib
+    monkeypatch.setenv("TD3_DP_BUCKETS", "2")
+    S = featured_setup_dims(376, 17, 0.4, "layer", B=1024)
+    pol, rb = _make(S)
+    uid = (C.c_ubyte * 128)()
+    _lib.check(pol._lib.td3_comm_unique_id(uid), "td3_comm_unique_id")
+    _lib.check(pol._lib.td3_comm_init(pol._h, uid, 1, 0), "td3_comm_init")
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    rs = np.random.RandomState(17)
+    for step in (1, 2):
+        idx = rs.randint(0, gen.BUFFER_ROWS, S["B"])
+        noise = rs.standard_normal((S["B"], S["ad"])).astype(np.float32)
+        _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        out = pol.train_step(rb, S["B"], indices=idx, noise=noise, stats=True)
+        assert _rel_to_max(out["y"], rec["y"][:, 0]) <= 1e-5, step
+        _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (step, "critic"))
+        _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
+        _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (step, "critic_target"))
+        st = pol.critic_optimizer.state_dict()["state"]
+        for i, k in enumerate(L.critic):
+            assert _rel_to_max(st[i]["exp_avg"].numpy(), L.critic_m[k]) <= 2e-4, (step, k)
+            assert _rel_to_max(st[i]["exp_avg_sq"].numpy(), L.critic_v[k]) <= 4e-4, (step, k)
+    ms = (C.c_float * 128)()
+    n = C.c_int()
+    _lib.check(pol._lib.td3_profile_stages(pol._h, rb.handle, S["B"], 1, ms, 128, C.byref(n)), "profile")
+    names = [pol._lib.td3_stage_name(pol._h, i).decode() for i in range(n.value)]
+    assert {"C_dw_0", "C_0_allreduce", "C_dw_1", "C_1_allreduce", "C_join"} <= set(names), names
+
+
 @pytest.mark.parametrize("sd,ad", [(24, 4), (29, 3)])
 def test_layer0_widths_teacher_forced(sd, ad):
     """Network inputs of 25..32 columns: the fused layer 0 runs its 16-MFMA K layout (inputs of

@@ -85,6 +85,10 @@ def main():
             v = buf[(buf[:, 3] != 0)].astype(np.int64)
             t0, t1, t2, t3 = v[:, 0], v[:, 1], v[:, 2], v[:, 3]
             base = t0.min()
+            if os.environ.get("TL_DUMP"):      # raw per-workgroup marks (rows = blockIdx with a mark)
+                os.makedirs(os.environ["TL_DUMP"], exist_ok=True)
+                np.save(os.path.join(os.environ["TL_DUMP"], f"p{phase}_{i:02d}_{name}.npy"),
+                        np.concatenate([np.nonzero(buf[:, 3] != 0)[0][:, None].astype(np.int64), v], axis=1))
             span = (t3.max() - base) * 0.01
             spread = (t0.max() - base) * 0.01
             clk = np.zeros((8192, 2), dtype=np.uint64)
