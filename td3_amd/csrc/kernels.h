@@ -253,6 +253,8 @@ struct DwSplit {
   const int* wg_unit;             // [G + 1]
   const int* tile_wg;             // [ntile][2]
   float* slab;                    // [G][J][slot]
+  int order;                      // 1: matrix steps step-major (dwsk_sm_kernel, tm = 64), 0: tile-major
+  int max_mat;                    // matrix tiles one workgroup range touches (order 1: <= kSmMat)
 };
 int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s);
 

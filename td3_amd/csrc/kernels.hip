@@ -2637,6 +2637,171 @@ __global__ __launch_bounds__(512, T128 ? 1 : 2) void dwsk_kernel(DwArgs a, DwSpl
 #endif
 }
 
+// Step-major order (round 4, 64 x 64 tiles; DwSplit::order = 1).  A workgroup's range touches up to
+// kSmMat matrix tiles (the tail of one, whole ones, the head of another).  dwsk_kernel walks them
+// tile by tile, so at any moment the 32 workgroups of an XCD stand at unrelated 64-row steps of
+// their panels, and the XCD's L2 has to keep whole dZ / U panels live between their first and last
+// reader: 3-4.7 MB of a 4 MB L2 at Humanoid C_dw (tools/sim_dwsk.py), hence the 58 % hit rate
+// (profiles/r03_pmc_humanoid.txt).  Here the matrix steps go step-major: for step s = 0..S-1, every
+// segment that holds step s, each into its own accumulator; the workgroups of an XCD then read the
+// same 64-row slices of their panels at about the same time (the live set falls to ~1 MB per XCD).
+// The vector segments follow afterwards (their operands are private to the tile: no reuse to lose),
+// and every partial lands where dwsk_kernel puts it, so dwsk_combine_kernel is unchanged.
+constexpr int kSmMat = 3;        // matrix segments per workgroup range (the planner checks, td3.hip)
+template <bool SC>
+__device__ __forceinline__ void dwsk_matrix_sm(const DwArgs& a, const DwSplit& k, int v, int u0, int u1,
+                                               float* sm) {
+  float* const ssl = sm + 2 * 2 * 64 * 64;
+  const int S = k.S, t0 = u0 / S;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
+  const int lr = lane >> 4, lc = (lane & 15) * 4;
+  // the matrix segments in range order: tile, steps [sb, se); uniform values
+  int tq[kSmMat], sbq[kSmMat], seq[kSmMat], nm = 0;
+  for (int t = t0; t <= (u1 - 1) / S && nm < kSmMat; ++t) {
+    const DwTile T = k.tiles[t];
+    if (__builtin_amdgcn_readfirstlane(T.kind) != 0) continue;
+    const int sb = t == t0 ? u0 - t * S : 0;
+    const int se = (u1 - t * S) < S ? u1 - t * S : S;
+#pragma unroll
+    for (int q = 0; q < kSmMat; ++q)
+      if (q == nm) {
+        tq[q] = t;
+        sbq[q] = sb;
+        seq[q] = se;
+      }
+    ++nm;
+  }
+  if (nm == 0) return;
+  // per segment: problem, tile origin, this lane's DMA source columns, live quadrant
+  auto seg = [&](int q, const DwProb*& P, int& n0, int& k0) {
+    const int t = __builtin_amdgcn_readfirstlane(q == 0 ? tq[0] : q == 1 ? tq[1] : tq[2]);
+    const DwTile T = k.tiles[t];
+    P = &a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
+    n0 = __builtin_amdgcn_readfirstlane(T.a) * 64;
+    k0 = __builtin_amdgcn_readfirstlane(T.b) * 64;
+  };
+  auto issue = [&](int q, int st, int buf) {
+    const DwProb* P;
+    int n0, k0;
+    seg(q, P, n0, k0);
+    float* g = sm + buf * 2 * 4096;
+    float* u = g + 4096;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 8 * wave + 4 * j + lr;
+      const int c = lc ^ (((row >> 4) & 1) << 5);
+      const int gc = min(n0 + c, P->Np - 4), uc = min(k0 + c, P->Kp - 4);
+      const int rl = 8 * wave + 4 * j;
+      const size_t grow = (size_t)(st * 64 + rl + lr);
+      glds16(P->G + grow * P->ldg + gc, g + rl * 64);
+      glds16(P->U + grow * P->ldu + uc, u + rl * 64);
+    }
+    if constexpr (SC) {
+      if (wave == 0) glds4(P->rs + (size_t)(st * 64 + lane) * P->ldrs, ssl + buf * 64);
+    }
+  };
+  // the unit after (s, q) in step-major order (s = S: none)
+  auto next = [&](int& s, int& q) {
+    do {
+      if (++q == nm) {
+        q = 0;
+        ++s;
+      }
+    } while (s < S && !(s >= (q == 0 ? sbq[0] : q == 1 ? sbq[1] : sbq[2]) &&
+                        s < (q == 0 ? seq[0] : q == 1 ? seq[1] : seq[2])));
+  };
+  f32x16 acc[kSmMat];
+#pragma unroll
+  for (int q = 0; q < kSmMat; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
+  int s = 0, q = -1;
+  q = nm - 1;
+  s = -1;
+  next(s, q);                                        // the first unit
+  int buf = 0;
+  issue(q, s, 0);
+  while (s < S) {
+    int s2 = s, q2 = q;
+    next(s2, q2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of (s, q) has landed
+    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
+    if (s2 < S) issue(q2, s2, buf ^ 1);
+    const DwProb* P;
+    int n0, k0;
+    seg(q, P, n0, k0);
+    const bool live = n0 + qn * 32 < P->Np && k0 + qk * 32 < P->Kp;
+    if (live) {
+      const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
+      const float* u = g + 4096;
+      float scl[16];
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * c4)
+                             : make_float4(1.f, 1.f, 1.f, 1.f);
+        scl[4 * c4 + 0] = v4.x; scl[4 * c4 + 1] = v4.y; scl[4 * c4 + 2] = v4.z; scl[4 * c4 + 3] = v4.w;
+      }
+#pragma unroll
+      for (int qq = 0; qq < kSmMat; ++qq) {
+        if (qq != q) continue;
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2) {
+          const float ga = g[r2 * 64 + ca];
+          acc[qq] = mfma32x32x2(SC ? ga * scl[r2] : ga, u[r2 * 64 + cb], acc[qq]);
+        }
+      }
+    }
+    buf ^= 1;
+    s = s2;
+    q = q2;
+  }
+  __syncthreads();                                   // staging buffers become the reduction tiles
+#pragma unroll
+  for (int qq = 0; qq < kSmMat; ++qq) {
+    if (qq >= nm) break;
+    const int t = tq[qq];
+    float* out = k.slab + ((size_t)v * k.J + (t - t0)) * k.slot;
+    float* red = sm + (wave & 3) * 32 * 33;
+    if (rh == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[qq][r];
+    }
+    __syncthreads();
+    if (rh == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        gst(out + (qn * 32 + mfma_row(r, lane)) * 64 + qk * 32 + i, acc[qq][r] + red[mfma_row(r, lane) * 33 + i]);
+    }
+    __syncthreads();
+  }
+}
+
+template <bool SC>
+__global__ __launch_bounds__(512, 2) void dwsk_sm_kernel(DwArgs a, DwSplit k) {
+  __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64];    // one __shared__ object (dwsk_kernel)
+  const int v = dwsk_virtual((int)blockIdx.x, k.G);
+  const int u0 = k.wg_unit[v], u1 = k.wg_unit[v + 1];
+  if (u0 >= u1) return;
+  dwsk_matrix_sm<SC>(a, k, v, u0, u1, sm);
+  // the vector segments of the range, tile by tile as dwsk_kernel
+  int u = u0, j = 0;
+  while (u < u1) {
+    const int t = __builtin_amdgcn_readfirstlane(u / k.S);
+    const int s0 = u - t * k.S;
+    const int s1 = (u1 - u) + s0 < k.S ? (u1 - u) + s0 : k.S;
+    const DwTile T = k.tiles[t];
+    if (__builtin_amdgcn_readfirstlane(T.kind) != 0) {
+      const DwProb& P = a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
+      dwsk_vector<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), s0, s1, sm,
+                      k.slab + ((size_t)v * k.J + j) * k.slot);
+    }
+    u += s1 - s0;
+    ++j;
+  }
+}
+
 // Four workgroups per tile (a quarter of a matrix tile's rows each; a vector tile uses the first):
 // the tile's partials summed in workgroup order, then the optimizer (or the gradient store of the
 // data-parallel / weight-norm paths) on its elements.
@@ -3098,6 +3263,9 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
   if (k.tm == 128) {
     if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, true>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_kernel<false, true>), dim3(k.G), dim3(512), 0, s, a, k);
+  } else if (k.order == 1) {
+    if (a.scaled) hipLaunchKernelGGL((dwsk_sm_kernel<true>), dim3(k.G), dim3(512), 0, s, a, k);
+    else hipLaunchKernelGGL((dwsk_sm_kernel<false>), dim3(k.G), dim3(512), 0, s, a, k);
   } else {
     if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_kernel<false, false>), dim3(k.G), dim3(512), 0, s, a, k);

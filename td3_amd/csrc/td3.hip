@@ -921,7 +921,15 @@ static int make_dw_split(td3_handle* h, std::vector<void*>& owned, const DwArgs&
     idx[k.G + 1 + 2 * t + 1] = vu[t * k.S + k.S - 1];
   }
   for (int v = 0; v < k.G; ++v)                 // partial slots: the tiles one workgroup's units touch
-    if (idx[v] < idx[v + 1]) k.J = std::max(k.J, (idx[v + 1] - 1) / k.S - idx[v] / k.S + 1);
+    if (idx[v] < idx[v + 1]) {
+      k.J = std::max(k.J, (idx[v + 1] - 1) / k.S - idx[v] / k.S + 1);
+      int nmat = 0;
+      for (int t = idx[v] / k.S; t <= (idx[v + 1] - 1) / k.S; ++t) nmat += tiles[t].kind == 0;
+      k.max_mat = std::max(k.max_mat, nmat);
+    }
+  // matrix steps step-major (dwsk_sm_kernel) when every range holds few enough matrix tiles;
+  // TD3_DWSK_ORDER=0 keeps the tile-major dwsk_kernel
+  k.order = (tm == 64 && k.max_mat <= 3 && env_int("TD3_DWSK_ORDER", 1) != 0) ? 1 : 0;
   void* d = nullptr;
   TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
   k.tiles = static_cast<const DwTile*>(d);
