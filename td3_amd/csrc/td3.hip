@@ -339,6 +339,7 @@ struct td3_handle {
   // last step that changed the online actor, so on critic-only steps (total_it % policy_freq != 0)
   // it overlaps the training step instead of queueing behind it.
   hipStream_t act_stream = nullptr;
+  hipEvent_t sync_ev = nullptr;               // td3_sync: the step stream's end, polled by the host
   hipEvent_t actor_ev = nullptr;              // recorded after every actor-updating step once a
                                               // query ran (act_used): an event record costs the
                                               // step's stream ~4 us, pure training needs none
@@ -2608,6 +2609,7 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   TD3_HIP(hipStreamCreateWithFlags(&h->act_stream, hipStreamNonBlocking));
   TD3_HIP(hipEventCreateWithFlags(&h->actor_ev, TD3_EV_FLAGS));
+  TD3_HIP(hipEventCreateWithFlags(&h->sync_ev, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -2640,6 +2642,7 @@ int td3_destroy(td3_handle* h) {
   (void)hipStreamSynchronize(h->act_stream);
   (void)hipStreamDestroy(h->act_stream);
   (void)hipEventDestroy(h->actor_ev);
+  (void)hipEventDestroy(h->sync_ev);
   (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -3229,11 +3232,23 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
   return 0;
 }
 
+// The host waits by polling an event recorded behind the queued steps: a blocking stream sync sleeps
+// on an interrupt once the wait grows long, and its wake-up added tens of us to the end of every
+// burst of steps (e.g. the 20-step timed runs of the driver's bench command).  One event record (a
+// marker packet) per call; the poll itself queues nothing.
 int td3_sync(td3_handle* h) {
   TD3_ARG(h != nullptr, "null handle");
   TD3_HIP(hipSetDevice(h->cfg.device));
-  TD3_HIP(hipStreamSynchronize(h->stream));
-  return 0;
+  TD3_HIP(hipEventRecord(h->sync_ev, h->stream));
+  for (;;) {
+    const hipError_t e = hipEventQuery(h->sync_ev);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) {
+      set_error("td3_sync: hipEventQuery: %s", hipGetErrorString(e));
+      return -2;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 void* td3_stream(td3_handle* h) { return h ? (void*)h->stream : nullptr; }
