@@ -2875,11 +2875,28 @@ __global__ __launch_bounds__(256) void dwsk_combine_kernel(DwArgs a, DwSplit k) 
   apply_grads<3>(a, make_adam(a.adam, pw), idx, gq, ok);
 }
 
+// The flat optimizer pass of the data-parallel path (after the all-reduce): 4 elements per thread
+// and array as one float4 (arenas and bucket ranges are multiples of 32 floats; launch_adam_flat
+// checks), every load of the 4 elements requested before the first store.
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, int polyak) {
   const AdamK k = make_adam(a);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float g = gld(a.G + (i)) * k.gscale;
-    adam_elem(a.P + i, a.M + i, a.V + i, g, k, polyak ? a.T + i : nullptr);
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = 4 * i;
+    const float4 g4 = gld4(a.G + e), m4 = gld4(a.M + e), v4 = gld4(a.V + e), p4 = gld4(a.P + e);
+    const float4 t4 = gld4((polyak ? a.T : a.P) + e);
+    float g[4] = {g4.x * k.gscale, g4.y * k.gscale, g4.z * k.gscale, g4.w * k.gscale};
+    float mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+    float pp[4] = {p4.x, p4.y, p4.z, p4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      adam_regs(pp[j], mm[j], vv[j], g[j], k);
+      tt[j] = k.tau * pp[j] + k.omt * tt[j];           // TD3_featured.py:167-171
+    }
+    gst4(a.M + e, make_float4(mm[0], mm[1], mm[2], mm[3]));
+    gst4(a.V + e, make_float4(vv[0], vv[1], vv[2], vv[3]));
+    gst4(a.P + e, make_float4(pp[0], pp[1], pp[2], pp[3]));
+    if (polyak) gst4(a.T + e, make_float4(tt[0], tt[1], tt[2], tt[3]));
   }
 }
 
@@ -3276,7 +3293,12 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
 }
 
 int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s) {
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  auto al16 = [](const float* p) { return ((uintptr_t)p & 15) == 0; };
+  if ((n & 3) || !al16(a.P) || !al16(a.G) || !al16(a.M) || !al16(a.V) || (polyak && !al16(a.T))) {
+    set_error("launch_adam_flat: the range must be float4-aligned (n %% 4 == 0, 16-B aligned arenas)");
+    return -1;
+  }
+  const int blocks = (int)std::min<int64_t>((n / 4 + 255) / 256, 2048);
   hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, a, n, polyak);
   TD3_HIP(hipGetLastError());
   return 0;
