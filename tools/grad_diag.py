@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Per-tensor Adam-moment errors against the oracle (GPU box diagnostic, not product code): the
+gradient-parity test's two steps at Humanoid widths, printing every tensor's relative error."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+
+from helpers import featured_setup_dims, gen, orc  # noqa: E402
+from test_gpu_parity import _load_oracle_state, _make, _rel_to_max  # noqa: E402
+
+
+def report(opt, m_ref, v_ref, what):
+    st = opt.state_dict()["state"]
+    bad = []
+    for i, k in enumerate(m_ref):
+        em = _rel_to_max(st[i]["exp_avg"].numpy(), m_ref[k])
+        ev = _rel_to_max(st[i]["exp_avg_sq"].numpy(), v_ref[k])
+        flag = "BAD" if em > 1e-4 else ""
+        print(f"  {what} {k:28s} m {em:.2e} v {ev:.2e} {flag}")
+        if flag:
+            bad.append(k)
+    return bad
+
+
+def main():
+    B = int(os.environ.get("DIAG_B", "1024"))
+    S = featured_setup_dims(376, 17, 0.4, "layer", B=B)
+    pol, rb = _make(S)
+    L = orc.Learner(S["actor"], S["critic"], **S["kw"])
+    rs = np.random.RandomState(11)
+    for step in (1, 2):
+        idx = rs.randint(0, gen.BUFFER_ROWS, size=B)
+        noise = rs.standard_normal((B, 17)).astype(np.float32)
+        if step == 2:
+            _load_oracle_state(pol, L)
+        rec = orc.featured_train_step(L, S["buf"].gather(idx), noise)
+        out = pol.train_step(rb, B, indices=idx, noise=noise, stats=True)
+        print(f"step {step}: y {_rel_to_max(out['y'], rec['y'][:, 0]):.2e} q1 {_rel_to_max(out['q1'], rec['q1'][:, 0]):.2e} "
+              f"q2 {_rel_to_max(out['q2'], rec['q2'][:, 0]):.2e}")
+        report(pol.critic_optimizer, L.critic_m, L.critic_v, f"critic s{step}")
+
+
+if __name__ == "__main__":
+    main()
