@@ -30,7 +30,7 @@ def report(opt, m_ref, v_ref, what):
 def main():
     B = int(os.environ.get("DIAG_B", "1024"))
     S = featured_setup_dims(376, 17, 0.4, "layer", B=B)
-    pol, rb = _make(S)
+    pol, rb = _make(S, use_graph=not os.environ.get("TD3_DIAG_EAGER"))
     L = orc.Learner(S["actor"], S["critic"], **S["kw"])
     rs = np.random.RandomState(11)
     for step in (1, 2):
