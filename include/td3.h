@@ -244,6 +244,12 @@ int td3_probe_kernel(td3_handle* h, rb_handle* rb, int batch, const char* kernel
                      int* launches);
 /* Algorithmic FLOPs of one launch of stage i (MFMA stages; 0 otherwise). */
 double td3_stage_flops(td3_handle* h, int i);
+/* Test instrumentation: the post-ReLU activations H_layer (layer 0..2) of one network evaluation of the
+ * last featured train step, rows x cols (cols <= the layer's width) into out (host, row-major).  eval:
+ * 0 target actor (s'), 1 Q1 (s, a), 2 Q2 (s, a), 3 actor (s), 4 / 5 target Q1 / Q2 (s', a'), 6 Q1 (s, pi).
+ * The tests take the ReLU masks of the step from it: where a pre-activation lies within fp32 rounding of
+ * zero the oracle and the GPU may both be right about opposite masks (tests/test_gpu_gradients.py). */
+int td3_debug_activation(td3_handle* h, int eval, int layer, float* out, int rows, int cols);
 
 const char* td3_last_error(void);
 

@@ -118,7 +118,9 @@ def mlp_forward(lin, ln, x):
 def mlp_backward(lin, ln, cache, gz_last):
     """Backward of ``mlp_forward`` given dL/d(last pre-activation).
 
-    Returns (grads in state-dict order pieces, dL/dx of the MLP input).
+    Returns (grads in state-dict order pieces, dL/dx of the MLP input).  ``cache["mask"]`` (optional,
+    one bool array per hidden layer) replaces the relu' masks h > 0: the GPU parity tests pass the
+    GPU's own masks, since a pre-activation within fp32 rounding of zero may fall on either side.
     """
     L = len(lin)
     gW = [None] * L
@@ -140,7 +142,8 @@ def mlp_backward(lin, ln, cache, gz_last):
             gh, gg[i - 1], gbeta[i - 1] = layernorm_bwd(gu, h, mean, rstd, ln[i - 1][0])
         else:
             gh = gu
-        gz = np.where(h > 0, gh, f32(0)).astype(f32)
+        mask = cache["mask"][i - 1] if "mask" in cache else h > 0
+        gz = np.where(mask, gh, f32(0)).astype(f32)
     raise AssertionError("unreachable")
 
 
@@ -300,14 +303,16 @@ def featured_q(P, q, norm, s, a):
     return z, (lin, ln, cache)
 
 
-def featured_train_step(L: Learner, batch, noise, record=None, grad_hook=None):
+def featured_train_step(L: Learner, batch, noise, record=None, grad_hook=None, masks=None):
     """One ``TD3_featured.TD3.train`` call (TD3_featured.py:123-171) on a gathered batch.
 
     ``batch`` = (state, action, next_state, reward, not_done) float32, ``noise`` =
     the N(0,1) draw of ``torch.randn_like(action)`` (:132).  ``grad_hook`` (data-parallel
     restatement) maps each phase's gradient dict before its Adam step, e.g. an
-    all-reduce mean over ranks that each hold one shard of the global batch.
+    all-reduce mean over ranks that each hold one shard of the global batch.  ``masks`` (tests):
+    relu' masks per network ("q1", "q2", "actor", "aq": lists of 3 bool arrays) for the backward.
     """
+    masks = masks or {}
     hook = grad_hook if grad_hook is not None else (lambda g: g)
     rec = record if record is not None else {}
     s, a, s2, r, nd = batch
@@ -328,25 +333,32 @@ def featured_train_step(L: Learner, batch, noise, record=None, grad_hook=None):
                critic_loss_parts=(l1, l2))
     grads = {}
     for q, qv, (lin, ln, cache) in (("q1", q1, c1), ("q2", q2, c2)):
+        if q in masks:
+            cache["mask"] = masks[q]
         gq = (f32(2.0 / (B)) * (qv - y)).astype(f32)                          # d mse / dQ
         g, _ = mlp_backward(lin, ln, cache, gq)
         grads.update(pack_mlp_grads(f"{q}.", g, L.norm, P=L.critic))
     rec["critic_grads"] = grads
     L.adam_critic(hook(grads))                                                 # :151-153
     if L.total_it % L.policy_freq == 0:                                        # :156
-        agrads = featured_actor_grads(L, s, rec)
+        agrads = featured_actor_grads(L, s, rec, masks)
         L.adam_actor(hook(agrads))                                             # :162-164
         L.polyak()                                                             # :167-171
     return rec
 
 
-def featured_actor_grads(L: Learner, s, record=None):
+def featured_actor_grads(L: Learner, s, record=None, masks=None):
     """The actor loss ``-Q1(s, pi(s)).mean()`` and its gradient over the actor's parameters
     (TD3_featured.py:159-161), with the critic as ``L.critic`` holds it (after the critic step)."""
     rec = record if record is not None else {}
     B = s.shape[0]
+    masks = masks or {}
     pi, (alin, aln, acache, t) = featured_actor(L.actor, L.norm, L.max_action, s)
     aq1, (qlin, qln, qcache) = featured_q(L.critic, "q1", L.norm, s, pi)       # :159
+    if "actor" in masks:
+        acache["mask"] = masks["actor"]
+    if "aq" in masks:
+        qcache["mask"] = masks["aq"]
     rec.update(pi=pi, actor_q1=aq1, actor_loss=-float(np.mean(aq1, dtype=np.float64)))
     gq = np.full((B, 1), -1.0 / B, dtype=f32)
     _, gx = mlp_backward(qlin, qln, qcache, gq)

@@ -3347,6 +3347,23 @@ int td3_probe_kernel(td3_handle* h, rb_handle* rb, int batch, const char* kernel
   return rc;
 }
 
+int td3_debug_activation(td3_handle* h, int eval, int layer, float* out, int rows, int cols) {
+  TD3_ARG(h && out, "null argument");
+  TD3_ARG(h->plan && !h->particles, "no featured plan (run a train step first)");
+  TD3_ARG(eval >= 0 && eval <= 6 && layer >= 0 && layer <= 2, "eval 0..6, layer 0..2");
+  Plan* P = h->plan.get();
+  const EvalB* ev[7] = {&P->TA, &P->Q[0], &P->Q[1], &P->A, &P->TQ[0], &P->TQ[1], &P->AQ};
+  const NetL& n = (eval == 0 || eval == 3) ? h->actor.nets[0] : h->critic.nets[(eval == 2 || eval == 5) ? 1 : 0];
+  const LinearL& L = n.lin[layer];
+  TD3_ARG(rows > 0 && rows <= P->Bp && cols > 0 && cols <= L.N, "rows / cols out of range");
+  TD3_ARG(ev[eval]->H[layer] != nullptr, "that activation is not kept by the plan");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  TD3_HIP(hipStreamSynchronize(h->stream));
+  TD3_HIP(hipMemcpy2D(out, (size_t)cols * 4, ev[eval]->H[layer], (size_t)L.Np * 4, (size_t)cols * 4, rows,
+                      hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int td3_time_stage(td3_handle* h, int stage, int iters, float* ms_mean) {
   TD3_ARG(h && ms_mean, "null argument");
   TD3_ARG(h->last_body != nullptr, "run td3_profile_stages first");
