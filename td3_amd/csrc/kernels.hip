@@ -2673,32 +2673,48 @@ __device__ __forceinline__ void dwsk_matrix_sm(const DwArgs& a, const DwSplit& k
     ++nm;
   }
   if (nm == 0) return;
-  // per segment: problem, tile origin, this lane's DMA source columns, live quadrant
-  auto seg = [&](int q, const DwProb*& P, int& n0, int& k0) {
-    const int t = __builtin_amdgcn_readfirstlane(q == 0 ? tq[0] : q == 1 ? tq[1] : tq[2]);
+  // per segment, loaded once: this lane's DMA sources (row 0 of the step), the operand row strides,
+  // the row-scale column and whether this wave's quadrant is live (edge tiles)
+  const float* gsrc[kSmMat][2];
+  const float* usrc[kSmMat][2];
+  const float* rsrc[kSmMat];
+  int ldg[kSmMat], ldu[kSmMat], ldr[kSmMat];
+  bool live[kSmMat];
+#pragma unroll
+  for (int qq = 0; qq < kSmMat; ++qq) {
+    const int t = __builtin_amdgcn_readfirstlane(qq < nm ? tq[qq] : tq[0]);
     const DwTile T = k.tiles[t];
-    P = &a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
-    n0 = __builtin_amdgcn_readfirstlane(T.a) * 64;
-    k0 = __builtin_amdgcn_readfirstlane(T.b) * 64;
-  };
-  auto issue = [&](int q, int st, int buf) {
-    const DwProb* P;
-    int n0, k0;
-    seg(q, P, n0, k0);
-    float* g = sm + buf * 2 * 4096;
-    float* u = g + 4096;
+    const DwProb& P = a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
+    const int n0 = __builtin_amdgcn_readfirstlane(T.a) * 64, k0 = __builtin_amdgcn_readfirstlane(T.b) * 64;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int row = 8 * wave + 4 * j + lr;
       const int c = lc ^ (((row >> 4) & 1) << 5);
-      const int gc = min(n0 + c, P->Np - 4), uc = min(k0 + c, P->Kp - 4);
-      const int rl = 8 * wave + 4 * j;
-      const size_t grow = (size_t)(st * 64 + rl + lr);
-      glds16(P->G + grow * P->ldg + gc, g + rl * 64);
-      glds16(P->U + grow * P->ldu + uc, u + rl * 64);
+      gsrc[qq][j] = P.G + (size_t)row * P.ldg + min(n0 + c, P.Np - 4);
+      usrc[qq][j] = P.U + (size_t)row * P.ldu + min(k0 + c, P.Kp - 4);
     }
-    if constexpr (SC) {
-      if (wave == 0) glds4(P->rs + (size_t)(st * 64 + lane) * P->ldrs, ssl + buf * 64);
+    rsrc[qq] = P.rs + (size_t)lane * P.ldrs;
+    ldg[qq] = P.ldg;
+    ldu[qq] = P.ldu;
+    ldr[qq] = P.ldrs;
+    live[qq] = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
+  }
+  auto issue = [&](int q, int st, int buf) {
+    float* g = sm + buf * 2 * 4096;
+    float* u = g + 4096;
+#pragma unroll
+    for (int qq = 0; qq < kSmMat; ++qq) {
+      if (qq != q) continue;
+      const size_t r0 = (size_t)st * 64;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rl = 8 * wave + 4 * j;
+        glds16(gsrc[qq][j] + r0 * ldg[qq], g + rl * 64);
+        glds16(usrc[qq][j] + r0 * ldu[qq], u + rl * 64);
+      }
+      if constexpr (SC) {
+        if (wave == 0) glds4(rsrc[qq] + r0 * ldr[qq], ssl + buf * 64);
+      }
     }
   };
   // the unit after (s, q) in step-major order (s = S: none)
@@ -2713,13 +2729,11 @@ __device__ __forceinline__ void dwsk_matrix_sm(const DwArgs& a, const DwSplit& k
   };
   f32x16 acc[kSmMat];
 #pragma unroll
-  for (int q = 0; q < kSmMat; ++q)
+  for (int qq = 0; qq < kSmMat; ++qq)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[qq][r] = 0.f;
   const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
-  int s = 0, q = -1;
-  q = nm - 1;
-  s = -1;
+  int q = nm - 1, s = -1;
   next(s, q);                                        // the first unit
   int buf = 0;
   issue(q, s, 0);
@@ -2729,28 +2743,22 @@ __device__ __forceinline__ void dwsk_matrix_sm(const DwArgs& a, const DwSplit& k
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of (s, q) has landed
     __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
     if (s2 < S) issue(q2, s2, buf ^ 1);
-    const DwProb* P;
-    int n0, k0;
-    seg(q, P, n0, k0);
-    const bool live = n0 + qn * 32 < P->Np && k0 + qk * 32 < P->Kp;
-    if (live) {
-      const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
-      const float* u = g + 4096;
-      float scl[16];
+    const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
+    const float* u = g + 4096;
+    float scl[16];
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * c4)
-                             : make_float4(1.f, 1.f, 1.f, 1.f);
-        scl[4 * c4 + 0] = v4.x; scl[4 * c4 + 1] = v4.y; scl[4 * c4 + 2] = v4.z; scl[4 * c4 + 3] = v4.w;
-      }
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * c4)
+                           : make_float4(1.f, 1.f, 1.f, 1.f);
+      scl[4 * c4 + 0] = v4.x; scl[4 * c4 + 1] = v4.y; scl[4 * c4 + 2] = v4.z; scl[4 * c4 + 3] = v4.w;
+    }
 #pragma unroll
-      for (int qq = 0; qq < kSmMat; ++qq) {
-        if (qq != q) continue;
+    for (int qq = 0; qq < kSmMat; ++qq) {
+      if (qq != q || !live[qq]) continue;
 #pragma unroll
-        for (int r2 = 0; r2 < 16; ++r2) {
-          const float ga = g[r2 * 64 + ca];
-          acc[qq] = mfma32x32x2(SC ? ga * scl[r2] : ga, u[r2 * 64 + cb], acc[qq]);
-        }
+      for (int r2 = 0; r2 < 16; ++r2) {
+        const float ga = g[r2 * 64 + ca];
+        acc[qq] = mfma32x32x2(SC ? ga * scl[r2] : ga, u[r2 * 64 + cb], acc[qq]);
       }
     }
     buf ^= 1;
