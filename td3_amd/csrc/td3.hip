@@ -928,9 +928,10 @@ static int make_dw_split(td3_handle* h, std::vector<void*>& owned, const DwArgs&
       for (int t = idx[v] / k.S; t <= (idx[v + 1] - 1) / k.S; ++t) nmat += tiles[t].kind == 0;
       k.max_mat = std::max(k.max_mat, nmat);
     }
-  // matrix steps step-major (dwsk_sm_kernel) when every range holds few enough matrix tiles;
-  // TD3_DWSK_ORDER=0 keeps the tile-major dwsk_kernel
-  k.order = (tm == 64 && k.max_mat <= 3 && env_int("TD3_DWSK_ORDER", 1) != 0) ? 1 : 0;
+  // matrix steps step-major (dwsk_sm_kernel, TD3_DWSK_ORDER=1) when every range holds few enough
+  // matrix tiles.  Measured slower (Humanoid C_dw 43.9 -> 49.6 us, A_dw 26.2 -> 29.2 us):
+  // the tile-major dwsk_kernel is the default
+  k.order = (tm == 64 && k.max_mat <= 3 && env_int("TD3_DWSK_ORDER", 0) != 0) ? 1 : 0;
   void* d = nullptr;
   TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
   k.tiles = static_cast<const DwTile*>(d);

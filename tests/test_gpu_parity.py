@@ -414,7 +414,7 @@ def test_split_dw_walk_orders_bitwise_equal(monkeypatch):
     draws = [(rs.randint(0, gen.BUFFER_ROWS, S["B"]), rs.standard_normal((S["B"], S["ad"])).astype(np.float32))
              for _ in range(2)]
     outs = []
-    for order in ("1", "0"):
+    for order in ("1", "0"):                   # (the step-major walk is opt-in: TD3_DWSK_ORDER=1)
         monkeypatch.setenv("TD3_DWSK_ORDER", order)
         pol, rb = _make(S)
         for idx, noise in draws:
