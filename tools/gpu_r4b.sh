@@ -17,3 +17,13 @@ for pass in "hf FETCH_SIZE" "hw WRITE_SIZE" "hl TCC_HIT_sum TCC_MISS_sum"; do
   timeout -s KILL 150 rocprofv3 --pmc $@ --output-format csv -d gpurun_out/pmc_${tag}_$name -o run -- python3 bench.py $H > gpurun_out/pmc_${tag}_$name.log 2>&1 || { echo "pmc $name failed"; tail -3 gpurun_out/pmc_${tag}_$name.log; exit 1; }
   echo "pmc $name ok"
 done
+timeout -k 10 200 python3 bench.py --dp-self --no-cpu-baseline --runs 3 > gpurun_out/bench_${tag}_dpself.json 2> gpurun_out/bench_${tag}_dpself.err || { echo dpself failed; tail -5 gpurun_out/bench_${tag}_dpself.err; exit 1; }
+echo "dpself ok: $(cut -c1-160 gpurun_out/bench_${tag}_dpself.json)"
+timeout -k 10 200 python3 bench.py --config humanoid --dp-self --no-cpu-baseline --runs 3 > gpurun_out/bench_${tag}_hdpself.json 2> gpurun_out/bench_${tag}_hdpself.err || { echo hdpself failed; exit 1; }
+echo "hdpself ok: $(cut -c1-160 gpurun_out/bench_${tag}_hdpself.json)"
+timeout -k 10 200 env TD3_DP_BUCKETS=2 python3 bench.py --config humanoid --dp-self --no-cpu-baseline --runs 3 > gpurun_out/bench_${tag}_hdpself_b.json 2> gpurun_out/bench_${tag}_hdpself_b.err || { echo hdpself_b failed; exit 1; }
+echo "hdpself buckets ok: $(cut -c1-160 gpurun_out/bench_${tag}_hdpself_b.json)"
+for i in 1 2 3; do
+  timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_${tag}_driver$i.json 2> gpurun_out/bench_${tag}_driver$i.err || { echo driver failed; exit 1; }
+  echo "driver form $i: $(cut -c1-200 gpurun_out/bench_${tag}_driver$i.json)"
+done
