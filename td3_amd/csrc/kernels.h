@@ -255,6 +255,7 @@ struct DwSplit {
   float* slab;                    // [G][J][slot]
   int order;                      // 1: matrix steps step-major (dwsk_sm_kernel, tm = 64), 0: tile-major
   int max_mat;                    // matrix tiles one workgroup range touches (order 1: <= kSmMat)
+  int depth;                      // tm = 64, order 0: LDS ring depth of the operand steps (2, 3, 4)
 };
 int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s);
 

@@ -2359,10 +2359,27 @@ __global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
 __device__ __forceinline__ int dwsk_virtual(int g, int G) { return (g & 7) * (G >> 3) + (g >> 3); }
 
 // Steps [s0, s1) of matrix tile (nt, kt) of P -> the 64x64 partial (row n - n0, column k - k0) at out.
-template <bool SC>
+// vmcnt(n) for a wave-uniform n < 16 (the immediate must be a constant)
+__device__ __forceinline__ void vm_wait_upto(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// NB: LDS ring depth (steps staged at once; NB - 1 DMA steps in flight while one is multiplied).
+// At NB = 2 one step is in flight behind the step being multiplied: a workgroup then waits a whole
+// DMA round trip per step whenever the trip outlasts the 16-MFMA chain (Humanoid C_dw: 1.55 us per
+// step against 0.85 us of MFMA issue).  Deeper rings keep NB - 1 steps in flight; LDS NB x 32 KB.
+template <bool SC, int NB = 2>
 __device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, int nt, int kt, int s0, int s1,
                                             float* sm, float* out) {
-  float* const ssl = sm + 2 * 2 * 64 * 64;
+  static_assert(NB >= 2 && NB <= 4, "ring depth");
+  float* const ssl = sm + NB * 2 * 64 * 64;
   const int n0 = nt * 64, k0 = kt * 64;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
   const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
@@ -2392,14 +2409,21 @@ __device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, in
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  issue(s0, 0);
   const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
   const bool live = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
-  for (int st = s0; st < s1; ++st) {
-    const int buf = (st - s0) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step st has landed
-    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
-    if (st + 1 < s1) issue(st + 1, buf ^ 1);
+  const int n = s1 - s0;
+  // DMA instructions this wave issues per step (wave 0 also stages the row scales)
+  const int ops = (SC && wave == 0) ? 5 : 4;
+#pragma unroll
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < n) issue(s0 + p, p);
+  for (int q = 0; q < n; ++q) {
+    const int st = s0 + q, buf = q % NB;
+    // this wave's DMA of step st has landed (the steps issued after it may stay in flight)
+    if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else vm_wait_upto(__builtin_amdgcn_readfirstlane(min(NB - 2, n - 1 - q) * ops));
+    __syncthreads();                                 // everyone's has; buffer (q - 1) % NB is free
+    if (q + NB - 1 < n) issue(st + NB - 1, (q + NB - 1) % NB);
     if (!live) continue;
     const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
     const float* u = g + 4096;
@@ -2590,11 +2614,11 @@ __device__ __forceinline__ void dwsk_vector(const DwArgs& a, const DwProb& P, in
   __syncthreads();
 }
 
-template <bool SC, bool T128>
-__global__ __launch_bounds__(512, T128 ? 1 : 2) void dwsk_kernel(DwArgs a, DwSplit k) {
+template <bool SC, bool T128, int NB = 2>
+__global__ __launch_bounds__(512, (T128 || NB > 2) ? 1 : 2) void dwsk_kernel(DwArgs a, DwSplit k) {
   // ONE __shared__ object (a second one made hipcc drain the DMA before every step's first operand
   // read, dw64g_kernel): [buf][operand][64 rows][tm cols (swizzled)], then SC's [buf][64] row scales
-  __shared__ float sm[2 * 2 * 64 * (T128 ? 128 : 64) + 2 * 64];
+  __shared__ float sm[NB * 2 * 64 * (T128 ? 128 : 64) + NB * 64];
   const int v = dwsk_virtual((int)blockIdx.x, k.G);
   TL_MARK(0);
   int u = k.wg_unit[v];
@@ -2614,7 +2638,7 @@ __global__ __launch_bounds__(512, T128 ? 1 : 2) void dwsk_kernel(DwArgs a, DwSpl
     const int ta = __builtin_amdgcn_readfirstlane(T.a);
     if (__builtin_amdgcn_readfirstlane(T.kind) == 0) {
       if constexpr (T128) dwsk_matrix128<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
-      else dwsk_matrix<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
+      else dwsk_matrix<SC, NB>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
     } else {
       dwsk_vector<SC>(a, P, ta, s0, s1, sm, out);
     }
@@ -3291,6 +3315,12 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
   } else if (k.order == 1) {
     if (a.scaled) hipLaunchKernelGGL((dwsk_sm_kernel<true>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_sm_kernel<false>), dim3(k.G), dim3(512), 0, s, a, k);
+  } else if (k.depth == 4) {
+    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);
+    else hipLaunchKernelGGL((dwsk_kernel<false, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);
+  } else if (k.depth == 3) {
+    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 3>), dim3(k.G), dim3(512), 0, s, a, k);
+    else hipLaunchKernelGGL((dwsk_kernel<false, false, 3>), dim3(k.G), dim3(512), 0, s, a, k);
   } else {
     if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_kernel<false, false>), dim3(k.G), dim3(512), 0, s, a, k);
