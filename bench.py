@@ -221,6 +221,9 @@ def roofline_from_stages(rows, pmc, probe=None):
         out["stage_kernels"] = [dom, "td3::dwsk_combine_kernel"]
         out["timing"] += ("; the split-K dW stage is two launches (partial tiles, then the fixed-order "
                           "combine with Adam), timed together and charged with the stage's FLOPs")
+        kern = (pmc or {}).get("kernels", {})
+        if all(k in kern for k in out["stage_kernels"]):      # the stage's traffic: both launches
+            out["traffic"] = sum(kern[k].get("hbm_bytes_per_launch", 0) for k in out["stage_kernels"])
     if probe and probe["launches"] > 0:
         in_step_s = probe["ms_total"] / probe["launches"] * 1e-3
         out["in_step_launch_us"] = round(in_step_s * 1e6, 3)

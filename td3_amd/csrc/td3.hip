@@ -932,8 +932,9 @@ static int make_dw_split(td3_handle* h, std::vector<void*>& owned, const DwArgs&
   // matrix tiles.  Measured slower (Humanoid C_dw 43.9 -> 49.6 us, A_dw 26.2 -> 29.2 us):
   // the tile-major dwsk_kernel is the default
   k.order = (tm == 64 && k.max_mat <= 3 && env_int("TD3_DWSK_ORDER", 0) != 0) ? 1 : 0;
-  // LDS ring depth of the tile-major walk: NB - 1 operand steps in flight
-  k.depth = std::min(4, std::max(2, env_int("TD3_DWSK_DEPTH", 4)));
+  // LDS ring depth of the tile-major walk: NB - 1 operand steps in flight.  Deeper rings measured
+  // slower (Humanoid C_dw 43.9 / 46.6 / 45.8 us at depth 2 / 3 / 4): 2 is the default
+  k.depth = std::min(4, std::max(2, env_int("TD3_DWSK_DEPTH", 2)));
   void* d = nullptr;
   TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
   k.tiles = static_cast<const DwTile*>(d);
