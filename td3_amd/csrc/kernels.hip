@@ -2834,6 +2834,157 @@ __global__ __launch_bounds__(512, 2) void dwsk_sm_kernel(DwArgs a, DwSplit k) {
   }
 }
 
+// Pipelined walk (round 4, 64 x 64 tiles, DwSplit::order = 2).  In dwsk_kernel every segment of a
+// range (the part of one tile the range holds) starts cold: the tile record and the problem's
+// fields are two dependent scalar round trips, the first operand step is then requested and waited
+// for with nothing else in flight, and the partial's LDS reduction reuses the staging buffers, so
+// the next segment cannot be staged behind it.  Per-workgroup timelines (tools/tl_probe.py, Humanoid
+// C_dw) fit 1.45 us per matrix step, 0.33 per vector step and 1.3 us per segment.  Here the ring
+// runs across segments: the next segment's record and fields are read while the current one runs,
+// its first step is requested with the current one's last (or at the start of a vector segment,
+// whose loads do not touch the ring), and the reduction has an LDS region of its own.  Same steps,
+// same accumulation order, same partial slots: bitwise equal to dwsk_kernel.
+struct DwMatSeg {
+  const float* G;
+  const float* U;
+  const float* rs;
+  int ldg, ldu, ldrs, n0, k0, Np, Kp;
+  int gcol[2], ucol[2];                              // this lane's DMA source columns (swizzled)
+};
+__device__ __forceinline__ void dw_mat_seg(const DwProb& P, int nt, int kt, int wave, int lane, DwMatSeg& m) {
+  m.G = P.G; m.U = P.U; m.rs = P.rs;
+  m.ldg = P.ldg; m.ldu = P.ldu; m.ldrs = P.ldrs;
+  m.n0 = nt * 64; m.k0 = kt * 64; m.Np = P.Np; m.Kp = P.Kp;
+  const int lr = lane >> 4, lc = (lane & 15) * 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * wave + 4 * j + lr;
+    const int c = lc ^ (((row >> 4) & 1) << 5);
+    m.gcol[j] = min(m.n0 + c, m.Np - 4);
+    m.ucol[j] = min(m.k0 + c, m.Kp - 4);
+  }
+}
+template <bool SC>
+__device__ __forceinline__ void dw_mat_issue(const DwMatSeg& m, int st, float* sm, int buf, int wave, int lane) {
+  float* g = sm + buf * 2 * 4096;
+  float* u = g + 4096;
+  const int lr = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rl = 8 * wave + 4 * j;
+    const size_t row = (size_t)(st * 64 + rl + lr);
+    glds16(m.G + row * m.ldg + m.gcol[j], g + rl * 64);
+    glds16(m.U + row * m.ldu + m.ucol[j], u + rl * 64);
+  }
+  if constexpr (SC) {
+    if (wave == 0) glds4(m.rs + (size_t)(st * 64 + lane) * m.ldrs, sm + 2 * 2 * 4096 + buf * 64);
+  }
+}
+
+template <bool SC>
+__global__ __launch_bounds__(512, 1) void dwsk_pipe_kernel(DwArgs a, DwSplit k) {
+  // [buf][operand][64 rows][64 cols (swizzled)] | SC's [buf][64] row scales | reduction (the matrix
+  // epilogue's 4 x 32 x 33, dwsk_vector's 3 x 64 x 33)
+  __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64 + 3 * 64 * 33];
+  float* const ssl = sm + 2 * 2 * 4096;
+  float* const red = ssl + 2 * 64;
+  const int v = dwsk_virtual((int)blockIdx.x, k.G);
+  TL_MARK(0);
+  const int u0 = k.wg_unit[v], u1 = k.wg_unit[v + 1];
+  if (u0 >= u1) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
+  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
+  const int S = k.S;
+
+  // the current segment: tile t, steps [s0, s1), kind; a matrix segment's DMA descriptor in cm
+  int u = u0, j = 0, gstep = 0;
+  int t = __builtin_amdgcn_readfirstlane(u / S);
+  int s0 = u - t * S, s1 = min(S, s0 + (u1 - u));
+  DwTile T = k.tiles[t];
+  int kind = __builtin_amdgcn_readfirstlane(T.kind);
+  int pi = __builtin_amdgcn_readfirstlane(T.prob);
+  DwMatSeg cm;
+  if (kind == 0) {
+    dw_mat_seg(a.probs[pi], __builtin_amdgcn_readfirstlane(T.a), __builtin_amdgcn_readfirstlane(T.b), wave, lane, cm);
+    dw_mat_issue<SC>(cm, s0, sm, 0, wave, lane);
+  }
+  while (true) {
+    // the next segment's record, requested now (read in this segment's shadow)
+    const int un = u + (s1 - s0);
+    const bool has_next = un < u1;
+    const int tn = has_next ? t + 1 : t;
+    const DwTile Tn = k.tiles[tn];
+    float* const out = k.slab + ((size_t)v * k.J + j) * k.slot;
+    if (kind == 0) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const bool live = cm.n0 + qn * 32 < cm.Np && cm.k0 + qk * 32 < cm.Kp;
+      const int nkind = __builtin_amdgcn_readfirstlane(Tn.kind);
+      const bool pre = has_next && nkind == 0;        // stage the next matrix segment's first step
+      DwMatSeg nm;
+      if (pre)
+        dw_mat_seg(a.probs[__builtin_amdgcn_readfirstlane(Tn.prob)], __builtin_amdgcn_readfirstlane(Tn.a),
+                   __builtin_amdgcn_readfirstlane(Tn.b), wave, lane, nm);
+      for (int st = s0; st < s1; ++st, ++gstep) {
+        const int buf = gstep & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step st has landed
+        __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
+        if (st + 1 < s1) dw_mat_issue<SC>(cm, st + 1, sm, buf ^ 1, wave, lane);
+        else if (pre) dw_mat_issue<SC>(nm, 0, sm, buf ^ 1, wave, lane);
+        if (!live) continue;
+        const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
+        const float* uu = g + 4096;
+        float scl[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * q)
+                               : make_float4(1.f, 1.f, 1.f, 1.f);
+          scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+          const float ga = g[s2 * 64 + ca];
+          acc = mfma32x32x2(SC ? ga * scl[s2] : ga, uu[s2 * 64 + cb], acc);
+        }
+      }
+      float* rr = red + (wave & 3) * 32 * 33;
+      if (rh == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rr[mfma_row(r, lane) * 33 + i] = acc[r];
+      }
+      __syncthreads();
+      if (rh == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          gst(out + (qn * 32 + mfma_row(r, lane)) * 64 + qk * 32 + i, acc[r] + rr[mfma_row(r, lane) * 33 + i]);
+      }
+      __syncthreads();                                 // red is reused by the next segment
+      if (pre) cm = nm;
+    } else {
+      const DwProb& P = a.probs[pi];
+      const int nkind = __builtin_amdgcn_readfirstlane(Tn.kind);
+      if (has_next && nkind == 0) {                    // stage the next matrix segment's first step now
+        dw_mat_seg(a.probs[__builtin_amdgcn_readfirstlane(Tn.prob)], __builtin_amdgcn_readfirstlane(Tn.a),
+                   __builtin_amdgcn_readfirstlane(Tn.b), wave, lane, cm);
+        dw_mat_issue<SC>(cm, 0, sm, gstep & 1, wave, lane);
+      }
+      dwsk_vector<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), s0, s1, red, out);
+    }
+    if (!has_next) break;
+    u = un;
+    t = tn;
+    T = Tn;
+    kind = __builtin_amdgcn_readfirstlane(T.kind);
+    pi = __builtin_amdgcn_readfirstlane(T.prob);
+    s0 = 0;
+    s1 = min(S, u1 - u);
+    ++j;
+  }
+  TL_MARK(3);
+}
+
 // Four workgroups per tile (a quarter of a matrix tile's rows each; a vector tile uses the first):
 // the tile's partials summed in workgroup order, then the optimizer (or the gradient store of the
 // data-parallel / weight-norm paths) on its elements.
@@ -3315,6 +3466,9 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
   } else if (k.order == 1) {
     if (a.scaled) hipLaunchKernelGGL((dwsk_sm_kernel<true>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_sm_kernel<false>), dim3(k.G), dim3(512), 0, s, a, k);
+  } else if (k.order == 2) {
+    if (a.scaled) hipLaunchKernelGGL((dwsk_pipe_kernel<true>), dim3(k.G), dim3(512), 0, s, a, k);
+    else hipLaunchKernelGGL((dwsk_pipe_kernel<false>), dim3(k.G), dim3(512), 0, s, a, k);
   } else if (k.depth == 4) {
     if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_kernel<false, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);

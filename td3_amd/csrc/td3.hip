@@ -858,11 +858,13 @@ constexpr int kDwSplitWorkgroups = TD3_DWSK_G;   // one per CU of the MI355X
 static int dwsk_tile_edge() { return env_int("TD3_DWSK_T", 64) == 128 ? 128 : 64; }
 static int dwsk_matrix_weight() { return std::max(1, env_int("TD3_DWSK_WM", 6)); }
 
-// The overlapped (bucketed) data-parallel dW schedule: TD3_DP_BUCKETS = 0 off; 1 (default) for real
+// The overlapped (bucketed) data-parallel dW schedule: TD3_DP_BUCKETS = 0 (default) off; 1 for real
 // peers (RCCL, nranks > 1) and the in-process seam; 2 also on a one-rank communicator (bench.py
-// --dp-self: the schedule's price without peers).  Read when a plan is built.
+// --dp-self: the schedule's price without peers).  Off by default: splitting the critic's dW into
+// two half-size launches costs ~12 us of GPU time at Humanoid B = 1024, about what
+// bucket 0's exchange can hide behind dW_1.  Read when a plan is built.
 static bool dp_overlap(const td3_handle* h) {
-  const int m = env_int("TD3_DP_BUCKETS", 1);
+  const int m = env_int("TD3_DP_BUCKETS", 0);
   if (m <= 0) return false;
   if (h->local) return true;
   return h->comm && (h->nranks > 1 || m >= 2);
@@ -931,7 +933,9 @@ static int make_dw_split(td3_handle* h, std::vector<void*>& owned, const DwArgs&
   // matrix steps step-major (dwsk_sm_kernel, TD3_DWSK_ORDER=1) when every range holds few enough
   // matrix tiles.  Measured slower (Humanoid C_dw 43.9 -> 49.6 us, A_dw 26.2 -> 29.2 us):
   // the tile-major dwsk_kernel is the default
-  k.order = (tm == 64 && k.max_mat <= 3 && env_int("TD3_DWSK_ORDER", 0) != 0) ? 1 : 0;
+  // TD3_DWSK_ORDER=2: the pipelined walk (dwsk_pipe_kernel: the ring runs across segments)
+  const int ord = env_int("TD3_DWSK_ORDER", 0);
+  k.order = tm != 64 ? 0 : (ord == 1 && k.max_mat <= 3) ? 1 : ord == 2 ? 2 : 0;
   // LDS ring depth of the tile-major walk: NB - 1 operand steps in flight.  Deeper rings measured
   // slower (Humanoid C_dw 43.9 / 46.6 / 45.8 us at depth 2 / 3 / 4): 2 is the default
   k.depth = std::min(4, std::max(2, env_int("TD3_DWSK_DEPTH", 2)));
@@ -1045,13 +1049,15 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.scaled = unit_scale ? 1 : 0;
   const int tm = dwsk_tile_edge();
   const bool split = tile64 && Bp % 64 == 0 && TD3_DWSK;
-  if (dp && split && !wn && enc_nwg == 0 && items.size() >= 2 && dp_overlap(h)) {
-    // The overlapped data-parallel schedule, one bucket per network of the group in
-    // arena order: bucket k's split-K dW (gradient only) on the step stream, then -- on the comm
-    // stream, behind an event -- the all-reduce of the network's arena range and its Adam (+ Polyak),
-    // while the step stream already runs bucket k+1's dW.  One join before the next stage reads the
-    // parameters.  The in-process seam runs the same buckets: a fixed-order sum of the range, then
-    // the bucket's optimizer step (Stage::after), on its one stream.
+  if (dp && split && !wn && enc_nwg == 0 && items.size() == 2 && dp_overlap(h)) {
+    // The overlapped data-parallel schedule for a twin critic: one bucket per network
+    // in arena order.  Stages: dW_0 (split-K, gradient only; then an event on the step stream),
+    // dW_1, bucket 0's all-reduce + Adam (+ Polyak) on the comm stream behind that event, bucket 1's
+    // on the step stream, then the join (the step stream waits for the comm stream's Adam).
+    // Bucket 0's exchange runs under dW_1; dW_1 is enqueued before the host makes bucket 0's RCCL
+    // call, and the last bucket stays on the step stream, so neither costs a stream hop on the
+    // critical path.  The in-process seam runs the same buckets: a fixed-order sum of the range,
+    // then the bucket's optimizer step (Stage::after), on its one stream.
     const bool local = h->local != nullptr;
     ncclComm_t comm = h->comm;
     hipStream_t cs = h->comm_stream;
@@ -1061,6 +1067,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     const std::string kname = std::string("td3::dwsk_kernel<") + (unit_scale ? "true, " : "false, ") +
                               (tm == 128 ? "true>" : "false>");
     int p0 = 0;
+    std::vector<Stage> exch;                        // bucket b's exchange stage
     for (size_t b = 0; b < items.size(); ++b) {
       const NetL& n = *items[b].net;
       const int cnt = 4 + (n.lnin ? 1 : 0);
@@ -1074,12 +1081,15 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       p0 += cnt;
       DwSplit kb{};
       TD3_RC(make_dw_split(h, owned, ab, slab, kb));
+      const bool first = b == 0;
       const std::string bn = std::string(tag) + "_dw_" + std::to_string(b);
       st.push_back({bn,
                     [=](hipStream_t s) {
                       DwSplit kk = kb;
                       kk.slab = slab->p;
-                      return launch_dw_split(ab, kk, s);
+                      TD3_RC(launch_dw_split(ab, kk, s));
+                      if (first && !local) TD3_HIP(hipEventRecord(ev, s));
+                      return 0;
                     },
                     fb, kname});
       const int64_t off = n.enc_off >= 0 ? n.enc_off : n.lin[0].offW;
@@ -1092,30 +1102,31 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       ar.P += off; ar.G += off; ar.M += off; ar.V += off; ar.T += off;
       ar.grad_scale = 1.0f / (float)h->nranks;
       float* Gb = g.G + off;
-      st.push_back({std::string(tag) + "_" + std::to_string(b) + "_allreduce",
-                    [=](hipStream_t s) {
-                      if (local) {
-                        set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
-                        return -1;
-                      }
-                      TD3_HIP(hipEventRecord(ev, s));
-                      TD3_HIP(hipStreamWaitEvent(cs, ev, 0));
-                      ncclResult_t r = ncclAllReduce(Gb, Gb, (size_t)nb, ncclFloat, ncclSum, comm, cs);
-                      if (r != ncclSuccess) {
-                        set_error("ncclAllReduce: %s", ncclGetErrorString(r));
-                        return -2;
-                      }
-                      TD3_RC(launch_adam_flat(ar, nb, pol, cs));
-                      TD3_HIP(hipEventRecord(done, cs));
-                      return 0;
-                    },
-                    0, "rccl"});
-      Stage& cst = st.back();
-      cst.collective = which == 1 ? 0 : 1;
-      cst.coll_off = off;
-      cst.coll_n = nb;
-      cst.after = [=](hipStream_t s) { return launch_adam_flat(ar, nb, pol, s); };
+      Stage x{std::string(tag) + "_" + std::to_string(b) + "_allreduce",
+              [=](hipStream_t s) {
+                if (local) {
+                  set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
+                  return -1;
+                }
+                hipStream_t q = first ? cs : s;
+                if (first) TD3_HIP(hipStreamWaitEvent(cs, ev, 0));
+                ncclResult_t r = ncclAllReduce(Gb, Gb, (size_t)nb, ncclFloat, ncclSum, comm, q);
+                if (r != ncclSuccess) {
+                  set_error("ncclAllReduce: %s", ncclGetErrorString(r));
+                  return -2;
+                }
+                TD3_RC(launch_adam_flat(ar, nb, pol, q));
+                if (first) TD3_HIP(hipEventRecord(done, cs));
+                return 0;
+              },
+              0, "rccl"};
+      x.collective = which == 1 ? 0 : 1;
+      x.coll_off = off;
+      x.coll_n = nb;
+      x.after = [=](hipStream_t s) { return launch_adam_flat(ar, nb, pol, s); };
+      exch.push_back(x);
     }
+    for (auto& x : exch) st.push_back(x);          // dW_0, dW_1, exchange 0 (comm), exchange 1 (step)
     st.push_back({std::string(tag) + "_join",
                   [=](hipStream_t s) {
                     if (local) return 0;            // the seam ran the buckets on its stream

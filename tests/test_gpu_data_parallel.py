@@ -107,14 +107,17 @@ def test_local_replicas_equal_global_batch_step(name, n):
         assert all(q._counters() == (L.total_it, L.critic_step, L.actor_step) for q in pols)
 
 
-def test_c5_eight_replicas_global_batch_8192():
+@pytest.mark.parametrize("buckets", ["0", "1"])
+def test_c5_eight_replicas_global_batch_8192(buckets, monkeypatch):
     """BASELINE config 5 (Humanoid-v4, 8 x MI355X, 1024 rows per GPU = global batch 8192) through
     the product's data-parallel stage lists: 8 replicas of one process at Humanoid widths, each on
     its 1024-row shard (split-K grad-only dW at B >= 512, the fixed-order sum in place of RCCL's
     all-reduce, flat Adam with grad scale 1/8), against the oracle's ONE global-batch step at
-    B = 8192 (TD3_featured.py:148-164).  A critic-only and a policy step, teacher-forced."""
+    B = 8192 (TD3_featured.py:148-164; SURVEY §8e).  A critic-only and a policy step, teacher-forced;
+    with the critic as one exchange and as the overlapped schedule's two buckets (TD3_DP_BUCKETS)."""
     from helpers import featured_setup_dims
     from td3_amd.data_parallel import train_local
+    monkeypatch.setenv("TD3_DP_BUCKETS", buckets)
     n, b = 8, 1024
     S = featured_setup_dims(376, 17, 0.4, "layer", B=n * b, steps=2)
     pols, rbs = _replicas(S, n, _make)

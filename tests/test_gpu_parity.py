@@ -348,9 +348,9 @@ def test_allreduce_path_single_rank(name):
 
 
 def test_overlapped_allreduce_schedule_single_rank(monkeypatch):
-    """The overlapped data-parallel schedule (td3.hip add_dw_stage buckets: per-network split-K dW,
-    then the all-reduce of the network's arena range and its Adam on the comm stream, joined back
-    before the next stage) through RCCL at nranks = 1 (TD3_DP_BUCKETS=2 turns it on without peers):
+    """The overlapped data-parallel schedule (td3.hip add_dw_stage buckets: per-network split-K dW;
+    bucket 0's all-reduce and Adam on the comm stream behind dW_1, bucket 1's on the step stream,
+    joined back before the next stage) through RCCL at nranks = 1 (TD3_DP_BUCKETS=2 turns it on without peers):
     Humanoid widths at B = 1024, a critic-only and a policy step against the oracle, both Adam moments
     included."""
     import ctypes as C
@@ -381,7 +381,8 @@ def test_overlapped_allreduce_schedule_single_rank(monkeypatch):
     n = C.c_int()
     _lib.check(pol._lib.td3_profile_stages(pol._h, rb.handle, S["B"], 1, ms, 128, C.byref(n)), "profile")
     names = [pol._lib.td3_stage_name(pol._h, i).decode() for i in range(n.value)]
-    assert {"C_dw_0", "C_0_allreduce", "C_dw_1", "C_1_allreduce", "C_join"} <= set(names), names
+    want = ["C_dw_0", "C_dw_1", "C_0_allreduce", "C_1_allreduce", "C_join"]
+    assert [x for x in names if x in want] == want, names
 
 
 @pytest.mark.parametrize("sd,ad", [(24, 4), (29, 3)])
@@ -407,15 +408,15 @@ def test_layer0_widths_teacher_forced(sd, ad):
 
 def test_split_dw_walks_bitwise_equal(monkeypatch):
     """Every split-K dW walk accumulates a tile segment's steps in the same order: the step-major
-    walk (dwsk_sm_kernel, TD3_DWSK_ORDER=1) and the tile-major one at LDS ring depths 2, 3 and 4
-    (TD3_DWSK_DEPTH).  Humanoid widths at B = 1024, two steps (critic and policy), bitwise equal
+    walk (dwsk_sm_kernel, TD3_DWSK_ORDER=1), the tile-major one at LDS ring depths 2, 3 and 4
+    (TD3_DWSK_DEPTH) and the pipelined one (dwsk_pipe_kernel, TD3_DWSK_ORDER=2).  Humanoid widths at B = 1024, two steps (critic and policy), bitwise equal
     parameters and Adam moments (both variables are read at plan build)."""
     S = featured_setup_dims(376, 17, 0.4, "layer", B=1024)
     rs = np.random.RandomState(5)
     draws = [(rs.randint(0, gen.BUFFER_ROWS, S["B"]), rs.standard_normal((S["B"], S["ad"])).astype(np.float32))
              for _ in range(2)]
     outs = []
-    for order, depth in (("1", "2"), ("0", "2"), ("0", "3"), ("0", "4")):
+    for order, depth in (("1", "2"), ("0", "2"), ("0", "3"), ("0", "4"), ("2", "2")):
         monkeypatch.setenv("TD3_DWSK_ORDER", order)
         monkeypatch.setenv("TD3_DWSK_DEPTH", depth)
         pol, rb = _make(S)
