@@ -2899,6 +2899,9 @@ __global__ __launch_bounds__(512, 1) void dwsk_pipe_kernel(DwArgs a, DwSplit k) 
 
   // the current segment: tile t, steps [s0, s1), kind; a matrix segment's DMA descriptor in cm
   int u = u0, j = 0, gstep = 0;
+#ifdef TD3_TL
+  int nmat = 0, nvec = 0;
+#endif
   int t = __builtin_amdgcn_readfirstlane(u / S);
   int s0 = u - t * S, s1 = min(S, s0 + (u1 - u));
   DwTile T = k.tiles[t];
@@ -2972,6 +2975,12 @@ __global__ __launch_bounds__(512, 1) void dwsk_pipe_kernel(DwArgs a, DwSplit k) 
       }
       dwsk_vector<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), s0, s1, red, out);
     }
+#ifdef TD3_TL
+    if (kind == 0) nmat += s1 - s0;
+    else nvec += s1 - s0;
+    if (j == 0) TL_MARK(1);
+    if (j == 1) TL_MARK(2);
+#endif
     if (!has_next) break;
     u = un;
     t = tn;
@@ -2983,6 +2992,13 @@ __global__ __launch_bounds__(512, 1) void dwsk_pipe_kernel(DwArgs a, DwSplit k) 
     ++j;
   }
   TL_MARK(3);
+#ifdef TD3_TL
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    td3_tl[blockIdx.x][5] = nmat;
+    td3_tl[blockIdx.x][6] = nvec;
+    td3_tl[blockIdx.x][7] = j + 1;
+  }
+#endif
 }
 
 // Four workgroups per tile (a quarter of a matrix tile's rows each; a vector tile uses the first):
