@@ -2455,6 +2455,86 @@ __device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, in
   __syncthreads();                                   // the next segment restages sm
 }
 
+// dwsk_matrix with two 64-row steps staged per barrier (DwSplit::depth = 5, "pairs"): each buffer
+// holds two steps (64 KB; 128 KB for the two buffers), so the eight waves meet at a barrier once
+// per 32 MFMAs instead of once per 16.  Same accumulation order as dwsk_matrix: bitwise equal.
+template <bool SC>
+__device__ __forceinline__ void dwsk_matrix_pair(const DwArgs& a, const DwProb& P, int nt, int kt, int s0, int s1,
+                                                 float* sm, float* out) {
+  float* const ssl = sm + 2 * 2 * 2 * 4096;
+  const int n0 = nt * 64, k0 = kt * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
+  const int lr = lane >> 4, lc = (lane & 15) * 4;
+  int gcol[2], ucol[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * wave + 4 * j + lr;
+    const int c = lc ^ (((row >> 4) & 1) << 5);
+    gcol[j] = min(n0 + c, P.Np - 4);
+    ucol[j] = min(k0 + c, P.Kp - 4);
+  }
+  auto issue = [&](int st, int slot) {                // slot = 2 * buffer + half
+    float* g = sm + slot * 2 * 4096;
+    float* u = g + 4096;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rl = 8 * wave + 4 * j;
+      const size_t row = (size_t)(st * 64 + rl + lr);
+      glds16(P.G + row * P.ldg + gcol[j], g + rl * 64);
+      glds16(P.U + row * P.ldu + ucol[j], u + rl * 64);
+    }
+    if constexpr (SC) {
+      if (wave == 0) glds4(P.rs + (size_t)(st * 64 + lane) * P.ldrs, ssl + slot * 64);
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
+  const bool live = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
+  auto step = [&](int slot) {
+    const float* g = sm + slot * 2 * 4096 + (rh * 32 + 16 * h) * 64;
+    const float* u = g + 4096;
+    float scl[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + slot * 64 + rh * 32 + 16 * h + 4 * q)
+                           : make_float4(1.f, 1.f, 1.f, 1.f);
+      scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const float ga = g[s2 * 64 + ca];
+      acc = mfma32x32x2(SC ? ga * scl[s2] : ga, u[s2 * 64 + cb], acc);
+    }
+  };
+  issue(s0, 0);
+  if (s0 + 1 < s1) issue(s0 + 1, 1);
+  for (int st = s0, buf = 0; st < s1; st += 2, buf ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of steps st, st + 1 has landed
+    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
+    if (st + 2 < s1) issue(st + 2, 2 * (buf ^ 1));
+    if (st + 3 < s1) issue(st + 3, 2 * (buf ^ 1) + 1);
+    if (!live) continue;
+    step(2 * buf);
+    if (st + 1 < s1) step(2 * buf + 1);
+  }
+  __syncthreads();                                   // staging buffers become the reduction tile
+  float* red = sm + (wave & 3) * 32 * 33;
+  if (rh == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[r];
+  }
+  __syncthreads();
+  if (rh == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      gst(out + (qn * 32 + mfma_row(r, lane)) * 64 + qk * 32 + i, acc[r] + red[mfma_row(r, lane) * 33 + i]);
+  }
+  __syncthreads();                                   // the next segment restages sm
+}
+
 // Steps [s0, s1) of 128 x 128 matrix tile (nt, kt) of P -> the partial (row n - n0, column k - k0,
 // ld 128) at out; quadrants past Np / Kp are neither fetched, multiplied nor stored.  LDS per buffer
 // and operand: [64 rows][128 cols], the 32-column groups 2c and 2c+1 swapped on rows with bit 4 set
@@ -2614,11 +2694,12 @@ __device__ __forceinline__ void dwsk_vector(const DwArgs& a, const DwProb& P, in
   __syncthreads();
 }
 
-template <bool SC, bool T128, int NB = 2>
+template <bool SC, bool T128, int NB = 2>             // NB: ring depth; 5 = two steps per barrier (pairs)
 __global__ __launch_bounds__(512, (T128 || NB > 2) ? 1 : 2) void dwsk_kernel(DwArgs a, DwSplit k) {
   // ONE __shared__ object (a second one made hipcc drain the DMA before every step's first operand
   // read, dw64g_kernel): [buf][operand][64 rows][tm cols (swizzled)], then SC's [buf][64] row scales
-  __shared__ float sm[NB * 2 * 64 * (T128 ? 128 : 64) + NB * 64];
+  constexpr int kSlots = NB == 5 ? 4 : NB;
+  __shared__ float sm[kSlots * 2 * 64 * (T128 ? 128 : 64) + kSlots * 64];
   const int v = dwsk_virtual((int)blockIdx.x, k.G);
   TL_MARK(0);
   int u = k.wg_unit[v];
@@ -2638,6 +2719,7 @@ __global__ __launch_bounds__(512, (T128 || NB > 2) ? 1 : 2) void dwsk_kernel(DwA
     const int ta = __builtin_amdgcn_readfirstlane(T.a);
     if (__builtin_amdgcn_readfirstlane(T.kind) == 0) {
       if constexpr (T128) dwsk_matrix128<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
+      else if constexpr (NB == 5) dwsk_matrix_pair<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
       else dwsk_matrix<SC, NB>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
     } else {
       dwsk_vector<SC>(a, P, ta, s0, s1, sm, out);
@@ -2882,7 +2964,9 @@ __device__ __forceinline__ void dw_mat_issue(const DwMatSeg& m, int st, float* s
 }
 
 template <bool SC>
-__global__ __launch_bounds__(512, 1) void dwsk_pipe_kernel(DwArgs a, DwSplit k) {
+// (launch bounds: the ring and the reduction region fit one workgroup per CU; the <= 128 VGPR
+// budget of two keeps dwsk_vector's codegen as in dwsk_kernel, whose vector steps ran faster)
+__global__ __launch_bounds__(512, 2) void dwsk_pipe_kernel(DwArgs a, DwSplit k) {
   // [buf][operand][64 rows][64 cols (swizzled)] | SC's [buf][64] row scales | reduction (the matrix
   // epilogue's 4 x 32 x 33, dwsk_vector's 3 x 64 x 33)
   __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64 + 3 * 64 * 33];
@@ -3485,6 +3569,9 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
   } else if (k.order == 2) {
     if (a.scaled) hipLaunchKernelGGL((dwsk_pipe_kernel<true>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_pipe_kernel<false>), dim3(k.G), dim3(512), 0, s, a, k);
+  } else if (k.depth == 5) {
+    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 5>), dim3(k.G), dim3(512), 0, s, a, k);
+    else hipLaunchKernelGGL((dwsk_kernel<false, false, 5>), dim3(k.G), dim3(512), 0, s, a, k);
   } else if (k.depth == 4) {
     if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_kernel<false, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);

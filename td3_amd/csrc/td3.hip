@@ -938,7 +938,8 @@ static int make_dw_split(td3_handle* h, std::vector<void*>& owned, const DwArgs&
   k.order = tm != 64 ? 0 : (ord == 1 && k.max_mat <= 3) ? 1 : ord == 2 ? 2 : 0;
   // LDS ring depth of the tile-major walk: NB - 1 operand steps in flight.  Deeper rings measured
   // slower (Humanoid C_dw 43.9 / 46.6 / 45.8 us at depth 2 / 3 / 4): 2 is the default
-  k.depth = std::min(4, std::max(2, env_int("TD3_DWSK_DEPTH", 2)));
+  // (5: two 64-row steps staged per barrier, dwsk_matrix_pair)
+  k.depth = std::min(5, std::max(2, env_int("TD3_DWSK_DEPTH", 2)));
   void* d = nullptr;
   TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
   k.tiles = static_cast<const DwTile*>(d);

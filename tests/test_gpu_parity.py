@@ -416,7 +416,7 @@ def test_split_dw_walks_bitwise_equal(monkeypatch):
     draws = [(rs.randint(0, gen.BUFFER_ROWS, S["B"]), rs.standard_normal((S["B"], S["ad"])).astype(np.float32))
              for _ in range(2)]
     outs = []
-    for order, depth in (("1", "2"), ("0", "2"), ("0", "3"), ("0", "4"), ("2", "2")):
+    for order, depth in (("1", "2"), ("0", "2"), ("0", "3"), ("0", "4"), ("0", "5"), ("2", "2")):
         monkeypatch.setenv("TD3_DWSK_ORDER", order)
         monkeypatch.setenv("TD3_DWSK_DEPTH", depth)
         pol, rb = _make(S)
