@@ -253,10 +253,6 @@ struct DwSplit {
   const int* wg_unit;             // [G + 1]
   const int* tile_wg;             // [ntile][2]
   float* slab;                    // [G][J][slot]
-  int order;                      // tm = 64: 0 tile-major (dwsk_kernel), 1 step-major (dwsk_sm_kernel),
-                                  // 2 tile-major with the ring across segments (dwsk_pipe_kernel)
-  int max_mat;                    // matrix tiles one workgroup range touches (order 1: <= kSmMat)
-  int depth;                      // tm = 64, order 0: LDS ring depth of the operand steps (2, 3, 4)
 };
 int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s);
 

@@ -2359,27 +2359,10 @@ __global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
 __device__ __forceinline__ int dwsk_virtual(int g, int G) { return (g & 7) * (G >> 3) + (g >> 3); }
 
 // Steps [s0, s1) of matrix tile (nt, kt) of P -> the 64x64 partial (row n - n0, column k - k0) at out.
-// vmcnt(n) for a wave-uniform n < 16 (the immediate must be a constant)
-__device__ __forceinline__ void vm_wait_upto(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-// NB: LDS ring depth (steps staged at once; NB - 1 DMA steps in flight while one is multiplied).
-// At NB = 2 one step is in flight behind the step being multiplied: a workgroup then waits a whole
-// DMA round trip per step whenever the trip outlasts the 16-MFMA chain (Humanoid C_dw: 1.55 us per
-// step against 0.85 us of MFMA issue).  Deeper rings keep NB - 1 steps in flight; LDS NB x 32 KB.
-template <bool SC, int NB = 2>
+template <bool SC>
 __device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, int nt, int kt, int s0, int s1,
                                             float* sm, float* out) {
-  static_assert(NB >= 2 && NB <= 4, "ring depth");
-  float* const ssl = sm + NB * 2 * 64 * 64;
+  float* const ssl = sm + 2 * 2 * 64 * 64;
   const int n0 = nt * 64, k0 = kt * 64;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
   const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
@@ -2409,21 +2392,14 @@ __device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, in
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  issue(s0, 0);
   const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
   const bool live = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
-  const int n = s1 - s0;
-  // DMA instructions this wave issues per step (wave 0 also stages the row scales)
-  const int ops = (SC && wave == 0) ? 5 : 4;
-#pragma unroll
-  for (int p = 0; p < NB - 1; ++p)
-    if (p < n) issue(s0 + p, p);
-  for (int q = 0; q < n; ++q) {
-    const int st = s0 + q, buf = q % NB;
-    // this wave's DMA of step st has landed (the steps issued after it may stay in flight)
-    if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else vm_wait_upto(__builtin_amdgcn_readfirstlane(min(NB - 2, n - 1 - q) * ops));
-    __syncthreads();                                 // everyone's has; buffer (q - 1) % NB is free
-    if (q + NB - 1 < n) issue(st + NB - 1, (q + NB - 1) % NB);
+  for (int st = s0; st < s1; ++st) {
+    const int buf = (st - s0) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step st has landed
+    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
+    if (st + 1 < s1) issue(st + 1, buf ^ 1);
     if (!live) continue;
     const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
     const float* u = g + 4096;
@@ -2439,86 +2415,6 @@ __device__ __forceinline__ void dwsk_matrix(const DwArgs& a, const DwProb& P, in
       const float ga = g[s2 * 64 + ca];
       acc = mfma32x32x2(SC ? ga * scl[s2] : ga, u[s2 * 64 + cb], acc);
     }
-  }
-  __syncthreads();                                   // staging buffers become the reduction tile
-  float* red = sm + (wave & 3) * 32 * 33;
-  if (rh == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[r];
-  }
-  __syncthreads();
-  if (rh == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      gst(out + (qn * 32 + mfma_row(r, lane)) * 64 + qk * 32 + i, acc[r] + red[mfma_row(r, lane) * 33 + i]);
-  }
-  __syncthreads();                                   // the next segment restages sm
-}
-
-// dwsk_matrix with two 64-row steps staged per barrier (DwSplit::depth = 5, "pairs"): each buffer
-// holds two steps (64 KB; 128 KB for the two buffers), so the eight waves meet at a barrier once
-// per 32 MFMAs instead of once per 16.  Same accumulation order as dwsk_matrix: bitwise equal.
-template <bool SC>
-__device__ __forceinline__ void dwsk_matrix_pair(const DwArgs& a, const DwProb& P, int nt, int kt, int s0, int s1,
-                                                 float* sm, float* out) {
-  float* const ssl = sm + 2 * 2 * 2 * 4096;
-  const int n0 = nt * 64, k0 = kt * 64;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
-  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
-  const int lr = lane >> 4, lc = (lane & 15) * 4;
-  int gcol[2], ucol[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = 8 * wave + 4 * j + lr;
-    const int c = lc ^ (((row >> 4) & 1) << 5);
-    gcol[j] = min(n0 + c, P.Np - 4);
-    ucol[j] = min(k0 + c, P.Kp - 4);
-  }
-  auto issue = [&](int st, int slot) {                // slot = 2 * buffer + half
-    float* g = sm + slot * 2 * 4096;
-    float* u = g + 4096;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int rl = 8 * wave + 4 * j;
-      const size_t row = (size_t)(st * 64 + rl + lr);
-      glds16(P.G + row * P.ldg + gcol[j], g + rl * 64);
-      glds16(P.U + row * P.ldu + ucol[j], u + rl * 64);
-    }
-    if constexpr (SC) {
-      if (wave == 0) glds4(P.rs + (size_t)(st * 64 + lane) * P.ldrs, ssl + slot * 64);
-    }
-  };
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
-  const bool live = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
-  auto step = [&](int slot) {
-    const float* g = sm + slot * 2 * 4096 + (rh * 32 + 16 * h) * 64;
-    const float* u = g + 4096;
-    float scl[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + slot * 64 + rh * 32 + 16 * h + 4 * q)
-                           : make_float4(1.f, 1.f, 1.f, 1.f);
-      scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) {
-      const float ga = g[s2 * 64 + ca];
-      acc = mfma32x32x2(SC ? ga * scl[s2] : ga, u[s2 * 64 + cb], acc);
-    }
-  };
-  issue(s0, 0);
-  if (s0 + 1 < s1) issue(s0 + 1, 1);
-  for (int st = s0, buf = 0; st < s1; st += 2, buf ^= 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of steps st, st + 1 has landed
-    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
-    if (st + 2 < s1) issue(st + 2, 2 * (buf ^ 1));
-    if (st + 3 < s1) issue(st + 3, 2 * (buf ^ 1) + 1);
-    if (!live) continue;
-    step(2 * buf);
-    if (st + 1 < s1) step(2 * buf + 1);
   }
   __syncthreads();                                   // staging buffers become the reduction tile
   float* red = sm + (wave & 3) * 32 * 33;
@@ -2694,12 +2590,11 @@ __device__ __forceinline__ void dwsk_vector(const DwArgs& a, const DwProb& P, in
   __syncthreads();
 }
 
-template <bool SC, bool T128, int NB = 2>             // NB: ring depth; 5 = two steps per barrier (pairs)
-__global__ __launch_bounds__(512, (T128 || NB > 2) ? 1 : 2) void dwsk_kernel(DwArgs a, DwSplit k) {
+template <bool SC, bool T128>
+__global__ __launch_bounds__(512, T128 ? 1 : 2) void dwsk_kernel(DwArgs a, DwSplit k) {
   // ONE __shared__ object (a second one made hipcc drain the DMA before every step's first operand
   // read, dw64g_kernel): [buf][operand][64 rows][tm cols (swizzled)], then SC's [buf][64] row scales
-  constexpr int kSlots = NB == 5 ? 4 : NB;
-  __shared__ float sm[kSlots * 2 * 64 * (T128 ? 128 : 64) + kSlots * 64];
+  __shared__ float sm[2 * 2 * 64 * (T128 ? 128 : 64) + 2 * 64];
   const int v = dwsk_virtual((int)blockIdx.x, k.G);
   TL_MARK(0);
   int u = k.wg_unit[v];
@@ -2719,8 +2614,7 @@ __global__ __launch_bounds__(512, (T128 || NB > 2) ? 1 : 2) void dwsk_kernel(DwA
     const int ta = __builtin_amdgcn_readfirstlane(T.a);
     if (__builtin_amdgcn_readfirstlane(T.kind) == 0) {
       if constexpr (T128) dwsk_matrix128<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
-      else if constexpr (NB == 5) dwsk_matrix_pair<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
-      else dwsk_matrix<SC, NB>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
+      else dwsk_matrix<SC>(a, P, ta, __builtin_amdgcn_readfirstlane(T.b), s0, s1, sm, out);
     } else {
       dwsk_vector<SC>(a, P, ta, s0, s1, sm, out);
     }
@@ -2739,348 +2633,6 @@ __global__ __launch_bounds__(512, (T128 || NB > 2) ? 1 : 2) void dwsk_kernel(DwA
     td3_tl[blockIdx.x][5] = nmat;
     td3_tl[blockIdx.x][6] = nvec;
     td3_tl[blockIdx.x][7] = j;
-  }
-#endif
-}
-
-// Step-major order (round 4, 64 x 64 tiles; DwSplit::order = 1).  A workgroup's range touches up to
-// kSmMat matrix tiles (the tail of one, whole ones, the head of another).  dwsk_kernel walks them
-// tile by tile, so at any moment the 32 workgroups of an XCD stand at unrelated 64-row steps of
-// their panels, and the XCD's L2 has to keep whole dZ / U panels live between their first and last
-// reader: 3-4.7 MB of a 4 MB L2 at Humanoid C_dw (tools/sim_dwsk.py), hence the 58 % hit rate
-// (profiles/r03_pmc_humanoid.txt).  Here the matrix steps go step-major: for step s = 0..S-1, every
-// segment that holds step s, each into its own accumulator; the workgroups of an XCD then read the
-// same 64-row slices of their panels at about the same time (the live set falls to ~1 MB per XCD).
-// The vector segments follow afterwards (their operands are private to the tile: no reuse to lose),
-// and every partial lands where dwsk_kernel puts it, so dwsk_combine_kernel is unchanged.
-constexpr int kSmMat = 3;        // matrix segments per workgroup range (the planner checks, td3.hip)
-template <bool SC>
-__device__ __forceinline__ void dwsk_matrix_sm(const DwArgs& a, const DwSplit& k, int v, int u0, int u1,
-                                               float* sm) {
-  float* const ssl = sm + 2 * 2 * 64 * 64;
-  const int S = k.S, t0 = u0 / S;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
-  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
-  const int lr = lane >> 4, lc = (lane & 15) * 4;
-  // the matrix segments in range order: tile, steps [sb, se); uniform values
-  int tq[kSmMat], sbq[kSmMat], seq[kSmMat], nm = 0;
-  for (int t = t0; t <= (u1 - 1) / S && nm < kSmMat; ++t) {
-    const DwTile T = k.tiles[t];
-    if (__builtin_amdgcn_readfirstlane(T.kind) != 0) continue;
-    const int sb = t == t0 ? u0 - t * S : 0;
-    const int se = (u1 - t * S) < S ? u1 - t * S : S;
-#pragma unroll
-    for (int q = 0; q < kSmMat; ++q)
-      if (q == nm) {
-        tq[q] = t;
-        sbq[q] = sb;
-        seq[q] = se;
-      }
-    ++nm;
-  }
-  if (nm == 0) return;
-  // per segment, loaded once: this lane's DMA sources (row 0 of the step), the operand row strides,
-  // the row-scale column and whether this wave's quadrant is live (edge tiles)
-  const float* gsrc[kSmMat][2];
-  const float* usrc[kSmMat][2];
-  const float* rsrc[kSmMat];
-  int ldg[kSmMat], ldu[kSmMat], ldr[kSmMat];
-  bool live[kSmMat];
-#pragma unroll
-  for (int qq = 0; qq < kSmMat; ++qq) {
-    const int t = __builtin_amdgcn_readfirstlane(qq < nm ? tq[qq] : tq[0]);
-    const DwTile T = k.tiles[t];
-    const DwProb& P = a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
-    const int n0 = __builtin_amdgcn_readfirstlane(T.a) * 64, k0 = __builtin_amdgcn_readfirstlane(T.b) * 64;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = 8 * wave + 4 * j + lr;
-      const int c = lc ^ (((row >> 4) & 1) << 5);
-      gsrc[qq][j] = P.G + (size_t)row * P.ldg + min(n0 + c, P.Np - 4);
-      usrc[qq][j] = P.U + (size_t)row * P.ldu + min(k0 + c, P.Kp - 4);
-    }
-    rsrc[qq] = P.rs + (size_t)lane * P.ldrs;
-    ldg[qq] = P.ldg;
-    ldu[qq] = P.ldu;
-    ldr[qq] = P.ldrs;
-    live[qq] = n0 + qn * 32 < P.Np && k0 + qk * 32 < P.Kp;
-  }
-  auto issue = [&](int q, int st, int buf) {
-    float* g = sm + buf * 2 * 4096;
-    float* u = g + 4096;
-#pragma unroll
-    for (int qq = 0; qq < kSmMat; ++qq) {
-      if (qq != q) continue;
-      const size_t r0 = (size_t)st * 64;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int rl = 8 * wave + 4 * j;
-        glds16(gsrc[qq][j] + r0 * ldg[qq], g + rl * 64);
-        glds16(usrc[qq][j] + r0 * ldu[qq], u + rl * 64);
-      }
-      if constexpr (SC) {
-        if (wave == 0) glds4(rsrc[qq] + r0 * ldr[qq], ssl + buf * 64);
-      }
-    }
-  };
-  // the unit after (s, q) in step-major order (s = S: none)
-  auto next = [&](int& s, int& q) {
-    do {
-      if (++q == nm) {
-        q = 0;
-        ++s;
-      }
-    } while (s < S && !(s >= (q == 0 ? sbq[0] : q == 1 ? sbq[1] : sbq[2]) &&
-                        s < (q == 0 ? seq[0] : q == 1 ? seq[1] : seq[2])));
-  };
-  f32x16 acc[kSmMat];
-#pragma unroll
-  for (int qq = 0; qq < kSmMat; ++qq)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[qq][r] = 0.f;
-  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
-  int q = nm - 1, s = -1;
-  next(s, q);                                        // the first unit
-  int buf = 0;
-  issue(q, s, 0);
-  while (s < S) {
-    int s2 = s, q2 = q;
-    next(s2, q2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of (s, q) has landed
-    __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
-    if (s2 < S) issue(q2, s2, buf ^ 1);
-    const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
-    const float* u = g + 4096;
-    float scl[16];
-#pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) {
-      const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * c4)
-                           : make_float4(1.f, 1.f, 1.f, 1.f);
-      scl[4 * c4 + 0] = v4.x; scl[4 * c4 + 1] = v4.y; scl[4 * c4 + 2] = v4.z; scl[4 * c4 + 3] = v4.w;
-    }
-#pragma unroll
-    for (int qq = 0; qq < kSmMat; ++qq) {
-      if (qq != q || !live[qq]) continue;
-#pragma unroll
-      for (int r2 = 0; r2 < 16; ++r2) {
-        const float ga = g[r2 * 64 + ca];
-        acc[qq] = mfma32x32x2(SC ? ga * scl[r2] : ga, u[r2 * 64 + cb], acc[qq]);
-      }
-    }
-    buf ^= 1;
-    s = s2;
-    q = q2;
-  }
-  __syncthreads();                                   // staging buffers become the reduction tiles
-#pragma unroll
-  for (int qq = 0; qq < kSmMat; ++qq) {
-    if (qq >= nm) break;
-    const int t = tq[qq];
-    float* out = k.slab + ((size_t)v * k.J + (t - t0)) * k.slot;
-    float* red = sm + (wave & 3) * 32 * 33;
-    if (rh == 1) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) red[mfma_row(r, lane) * 33 + i] = acc[qq][r];
-    }
-    __syncthreads();
-    if (rh == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        gst(out + (qn * 32 + mfma_row(r, lane)) * 64 + qk * 32 + i, acc[qq][r] + red[mfma_row(r, lane) * 33 + i]);
-    }
-    __syncthreads();
-  }
-}
-
-template <bool SC>
-__global__ __launch_bounds__(512, 2) void dwsk_sm_kernel(DwArgs a, DwSplit k) {
-  __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64];    // one __shared__ object (dwsk_kernel)
-  const int v = dwsk_virtual((int)blockIdx.x, k.G);
-  const int u0 = k.wg_unit[v], u1 = k.wg_unit[v + 1];
-  if (u0 >= u1) return;
-  dwsk_matrix_sm<SC>(a, k, v, u0, u1, sm);
-  // the vector segments of the range, tile by tile as dwsk_kernel
-  int u = u0, j = 0;
-  while (u < u1) {
-    const int t = __builtin_amdgcn_readfirstlane(u / k.S);
-    const int s0 = u - t * k.S;
-    const int s1 = (u1 - u) + s0 < k.S ? (u1 - u) + s0 : k.S;
-    const DwTile T = k.tiles[t];
-    if (__builtin_amdgcn_readfirstlane(T.kind) != 0) {
-      const DwProb& P = a.probs[__builtin_amdgcn_readfirstlane(T.prob)];
-      dwsk_vector<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), s0, s1, sm,
-                      k.slab + ((size_t)v * k.J + j) * k.slot);
-    }
-    u += s1 - s0;
-    ++j;
-  }
-}
-
-// Pipelined walk (round 4, 64 x 64 tiles, DwSplit::order = 2).  In dwsk_kernel every segment of a
-// range (the part of one tile the range holds) starts cold: the tile record and the problem's
-// fields are two dependent scalar round trips, the first operand step is then requested and waited
-// for with nothing else in flight, and the partial's LDS reduction reuses the staging buffers, so
-// the next segment cannot be staged behind it.  Per-workgroup timelines (tools/tl_probe.py, Humanoid
-// C_dw) fit 1.45 us per matrix step, 0.33 per vector step and 1.3 us per segment.  Here the ring
-// runs across segments: the next segment's record and fields are read while the current one runs,
-// its first step is requested with the current one's last (or at the start of a vector segment,
-// whose loads do not touch the ring), and the reduction has an LDS region of its own.  Same steps,
-// same accumulation order, same partial slots: bitwise equal to dwsk_kernel.
-struct DwMatSeg {
-  const float* G;
-  const float* U;
-  const float* rs;
-  int ldg, ldu, ldrs, n0, k0, Np, Kp;
-  int gcol[2], ucol[2];                              // this lane's DMA source columns (swizzled)
-};
-__device__ __forceinline__ void dw_mat_seg(const DwProb& P, int nt, int kt, int wave, int lane, DwMatSeg& m) {
-  m.G = P.G; m.U = P.U; m.rs = P.rs;
-  m.ldg = P.ldg; m.ldu = P.ldu; m.ldrs = P.ldrs;
-  m.n0 = nt * 64; m.k0 = kt * 64; m.Np = P.Np; m.Kp = P.Kp;
-  const int lr = lane >> 4, lc = (lane & 15) * 4;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = 8 * wave + 4 * j + lr;
-    const int c = lc ^ (((row >> 4) & 1) << 5);
-    m.gcol[j] = min(m.n0 + c, m.Np - 4);
-    m.ucol[j] = min(m.k0 + c, m.Kp - 4);
-  }
-}
-template <bool SC>
-__device__ __forceinline__ void dw_mat_issue(const DwMatSeg& m, int st, float* sm, int buf, int wave, int lane) {
-  float* g = sm + buf * 2 * 4096;
-  float* u = g + 4096;
-  const int lr = lane >> 4;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int rl = 8 * wave + 4 * j;
-    const size_t row = (size_t)(st * 64 + rl + lr);
-    glds16(m.G + row * m.ldg + m.gcol[j], g + rl * 64);
-    glds16(m.U + row * m.ldu + m.ucol[j], u + rl * 64);
-  }
-  if constexpr (SC) {
-    if (wave == 0) glds4(m.rs + (size_t)(st * 64 + lane) * m.ldrs, sm + 2 * 2 * 4096 + buf * 64);
-  }
-}
-
-template <bool SC>
-// (launch bounds: the ring and the reduction region fit one workgroup per CU; the <= 128 VGPR
-// budget of two keeps dwsk_vector's codegen as in dwsk_kernel, whose vector steps ran faster)
-__global__ __launch_bounds__(512, 2) void dwsk_pipe_kernel(DwArgs a, DwSplit k) {
-  // [buf][operand][64 rows][64 cols (swizzled)] | SC's [buf][64] row scales | reduction (the matrix
-  // epilogue's 4 x 32 x 33, dwsk_vector's 3 x 64 x 33)
-  __shared__ float sm[2 * 2 * 64 * 64 + 2 * 64 + 3 * 64 * 33];
-  float* const ssl = sm + 2 * 2 * 4096;
-  float* const red = ssl + 2 * 64;
-  const int v = dwsk_virtual((int)blockIdx.x, k.G);
-  TL_MARK(0);
-  const int u0 = k.wg_unit[v], u1 = k.wg_unit[v + 1];
-  if (u0 >= u1) return;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
-  const int qn = (wave >> 1) & 1, qk = wave & 1, rh = wave >> 2;
-  const int ca = (qn ^ h) * 32 + i, cb = (qk ^ h) * 32 + i;
-  const int S = k.S;
-
-  // the current segment: tile t, steps [s0, s1), kind; a matrix segment's DMA descriptor in cm
-  int u = u0, j = 0, gstep = 0;
-#ifdef TD3_TL
-  int nmat = 0, nvec = 0;
-#endif
-  int t = __builtin_amdgcn_readfirstlane(u / S);
-  int s0 = u - t * S, s1 = min(S, s0 + (u1 - u));
-  DwTile T = k.tiles[t];
-  int kind = __builtin_amdgcn_readfirstlane(T.kind);
-  int pi = __builtin_amdgcn_readfirstlane(T.prob);
-  DwMatSeg cm;
-  if (kind == 0) {
-    dw_mat_seg(a.probs[pi], __builtin_amdgcn_readfirstlane(T.a), __builtin_amdgcn_readfirstlane(T.b), wave, lane, cm);
-    dw_mat_issue<SC>(cm, s0, sm, 0, wave, lane);
-  }
-  while (true) {
-    // the next segment's record, requested now (read in this segment's shadow)
-    const int un = u + (s1 - s0);
-    const bool has_next = un < u1;
-    const int tn = has_next ? t + 1 : t;
-    const DwTile Tn = k.tiles[tn];
-    float* const out = k.slab + ((size_t)v * k.J + j) * k.slot;
-    if (kind == 0) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const bool live = cm.n0 + qn * 32 < cm.Np && cm.k0 + qk * 32 < cm.Kp;
-      const int nkind = __builtin_amdgcn_readfirstlane(Tn.kind);
-      const bool pre = has_next && nkind == 0;        // stage the next matrix segment's first step
-      DwMatSeg nm;
-      if (pre)
-        dw_mat_seg(a.probs[__builtin_amdgcn_readfirstlane(Tn.prob)], __builtin_amdgcn_readfirstlane(Tn.a),
-                   __builtin_amdgcn_readfirstlane(Tn.b), wave, lane, nm);
-      for (int st = s0; st < s1; ++st, ++gstep) {
-        const int buf = gstep & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step st has landed
-        __syncthreads();                                 // everyone's has; buffer buf ^ 1 is free
-        if (st + 1 < s1) dw_mat_issue<SC>(cm, st + 1, sm, buf ^ 1, wave, lane);
-        else if (pre) dw_mat_issue<SC>(nm, 0, sm, buf ^ 1, wave, lane);
-        if (!live) continue;
-        const float* g = sm + buf * 2 * 4096 + (rh * 32 + 16 * h) * 64;
-        const float* uu = g + 4096;
-        float scl[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v4 = SC ? *reinterpret_cast<const float4*>(ssl + buf * 64 + rh * 32 + 16 * h + 4 * q)
-                               : make_float4(1.f, 1.f, 1.f, 1.f);
-          scl[4 * q + 0] = v4.x; scl[4 * q + 1] = v4.y; scl[4 * q + 2] = v4.z; scl[4 * q + 3] = v4.w;
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) {
-          const float ga = g[s2 * 64 + ca];
-          acc = mfma32x32x2(SC ? ga * scl[s2] : ga, uu[s2 * 64 + cb], acc);
-        }
-      }
-      float* rr = red + (wave & 3) * 32 * 33;
-      if (rh == 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) rr[mfma_row(r, lane) * 33 + i] = acc[r];
-      }
-      __syncthreads();
-      if (rh == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          gst(out + (qn * 32 + mfma_row(r, lane)) * 64 + qk * 32 + i, acc[r] + rr[mfma_row(r, lane) * 33 + i]);
-      }
-      __syncthreads();                                 // red is reused by the next segment
-      if (pre) cm = nm;
-    } else {
-      const DwProb& P = a.probs[pi];
-      const int nkind = __builtin_amdgcn_readfirstlane(Tn.kind);
-      if (has_next && nkind == 0) {                    // stage the next matrix segment's first step now
-        dw_mat_seg(a.probs[__builtin_amdgcn_readfirstlane(Tn.prob)], __builtin_amdgcn_readfirstlane(Tn.a),
-                   __builtin_amdgcn_readfirstlane(Tn.b), wave, lane, cm);
-        dw_mat_issue<SC>(cm, 0, sm, gstep & 1, wave, lane);
-      }
-      dwsk_vector<SC>(a, P, __builtin_amdgcn_readfirstlane(T.a), s0, s1, red, out);
-    }
-#ifdef TD3_TL
-    if (kind == 0) nmat += s1 - s0;
-    else nvec += s1 - s0;
-    if (j == 0) TL_MARK(1);
-    if (j == 1) TL_MARK(2);
-#endif
-    if (!has_next) break;
-    u = un;
-    t = tn;
-    T = Tn;
-    kind = __builtin_amdgcn_readfirstlane(T.kind);
-    pi = __builtin_amdgcn_readfirstlane(T.prob);
-    s0 = 0;
-    s1 = min(S, u1 - u);
-    ++j;
-  }
-  TL_MARK(3);
-#ifdef TD3_TL
-  if (threadIdx.x == 0 && blockIdx.x < 8192) {
-    td3_tl[blockIdx.x][5] = nmat;
-    td3_tl[blockIdx.x][6] = nvec;
-    td3_tl[blockIdx.x][7] = j + 1;
   }
 #endif
 }
@@ -3563,21 +3115,6 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
   if (k.tm == 128) {
     if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, true>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_kernel<false, true>), dim3(k.G), dim3(512), 0, s, a, k);
-  } else if (k.order == 1) {
-    if (a.scaled) hipLaunchKernelGGL((dwsk_sm_kernel<true>), dim3(k.G), dim3(512), 0, s, a, k);
-    else hipLaunchKernelGGL((dwsk_sm_kernel<false>), dim3(k.G), dim3(512), 0, s, a, k);
-  } else if (k.order == 2) {
-    if (a.scaled) hipLaunchKernelGGL((dwsk_pipe_kernel<true>), dim3(k.G), dim3(512), 0, s, a, k);
-    else hipLaunchKernelGGL((dwsk_pipe_kernel<false>), dim3(k.G), dim3(512), 0, s, a, k);
-  } else if (k.depth == 5) {
-    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 5>), dim3(k.G), dim3(512), 0, s, a, k);
-    else hipLaunchKernelGGL((dwsk_kernel<false, false, 5>), dim3(k.G), dim3(512), 0, s, a, k);
-  } else if (k.depth == 4) {
-    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);
-    else hipLaunchKernelGGL((dwsk_kernel<false, false, 4>), dim3(k.G), dim3(512), 0, s, a, k);
-  } else if (k.depth == 3) {
-    if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false, 3>), dim3(k.G), dim3(512), 0, s, a, k);
-    else hipLaunchKernelGGL((dwsk_kernel<false, false, 3>), dim3(k.G), dim3(512), 0, s, a, k);
   } else {
     if (a.scaled) hipLaunchKernelGGL((dwsk_kernel<true, false>), dim3(k.G), dim3(512), 0, s, a, k);
     else hipLaunchKernelGGL((dwsk_kernel<false, false>), dim3(k.G), dim3(512), 0, s, a, k);

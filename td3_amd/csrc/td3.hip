@@ -924,22 +924,7 @@ static int make_dw_split(td3_handle* h, std::vector<void*>& owned, const DwArgs&
     idx[k.G + 1 + 2 * t + 1] = vu[t * k.S + k.S - 1];
   }
   for (int v = 0; v < k.G; ++v)                 // partial slots: the tiles one workgroup's units touch
-    if (idx[v] < idx[v + 1]) {
-      k.J = std::max(k.J, (idx[v + 1] - 1) / k.S - idx[v] / k.S + 1);
-      int nmat = 0;
-      for (int t = idx[v] / k.S; t <= (idx[v + 1] - 1) / k.S; ++t) nmat += tiles[t].kind == 0;
-      k.max_mat = std::max(k.max_mat, nmat);
-    }
-  // matrix steps step-major (dwsk_sm_kernel, TD3_DWSK_ORDER=1) when every range holds few enough
-  // matrix tiles.  Measured slower (Humanoid C_dw 43.9 -> 49.6 us, A_dw 26.2 -> 29.2 us):
-  // the tile-major dwsk_kernel is the default
-  // TD3_DWSK_ORDER=2: the pipelined walk (dwsk_pipe_kernel: the ring runs across segments)
-  const int ord = env_int("TD3_DWSK_ORDER", 0);
-  k.order = tm != 64 ? 0 : (ord == 1 && k.max_mat <= 3) ? 1 : ord == 2 ? 2 : 0;
-  // LDS ring depth of the tile-major walk: NB - 1 operand steps in flight.  Deeper rings measured
-  // slower (Humanoid C_dw 43.9 / 46.6 / 45.8 us at depth 2 / 3 / 4): 2 is the default
-  // (5: two 64-row steps staged per barrier, dwsk_matrix_pair)
-  k.depth = std::min(5, std::max(2, env_int("TD3_DWSK_DEPTH", 2)));
+    if (idx[v] < idx[v + 1]) k.J = std::max(k.J, (idx[v + 1] - 1) / k.S - idx[v] / k.S + 1);
   void* d = nullptr;
   TD3_RC(upload(h, owned, tiles.data(), tiles.size() * sizeof(DwTile), &d));
   k.tiles = static_cast<const DwTile*>(d);

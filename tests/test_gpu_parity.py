@@ -406,29 +406,6 @@ def test_layer0_widths_teacher_forced(sd, ad):
         _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
 
 
-def test_split_dw_walks_bitwise_equal(monkeypatch):
-    """Every split-K dW walk accumulates a tile segment's steps in the same order: the step-major
-    walk (dwsk_sm_kernel, TD3_DWSK_ORDER=1), the tile-major one at LDS ring depths 2, 3 and 4
-    (TD3_DWSK_DEPTH) and the pipelined one (dwsk_pipe_kernel, TD3_DWSK_ORDER=2).  Humanoid widths at B = 1024, two steps (critic and policy), bitwise equal
-    parameters and Adam moments (both variables are read at plan build)."""
-    S = featured_setup_dims(376, 17, 0.4, "layer", B=1024)
-    rs = np.random.RandomState(5)
-    draws = [(rs.randint(0, gen.BUFFER_ROWS, S["B"]), rs.standard_normal((S["B"], S["ad"])).astype(np.float32))
-             for _ in range(2)]
-    outs = []
-    for order, depth in (("1", "2"), ("0", "2"), ("0", "3"), ("0", "4"), ("0", "5"), ("2", "2")):
-        monkeypatch.setenv("TD3_DWSK_ORDER", order)
-        monkeypatch.setenv("TD3_DWSK_DEPTH", depth)
-        pol, rb = _make(S)
-        for idx, noise in draws:
-            pol.train_step(rb, S["B"], indices=idx, noise=noise)
-        outs.append((pol.actor.flat(), pol.critic.flat(),
-                     pol.critic_optimizer.state_dict()["state"][0]["exp_avg_sq"].numpy()))
-    for other in outs[1:]:
-        for a, b in zip(outs[0], other):
-            np.testing.assert_array_equal(a, b)
-
-
 @pytest.mark.parametrize("B", [512, 1024])
 def test_large_batch_teacher_forced(B):
     """Batches >= 512 switch the wide stages to 128-column GEMM workgroups with the K chunks
