@@ -31,7 +31,7 @@ def main():
     from td3_amd.TD3_featured import TD3
     from td3_amd.my_replay_buffer import ReplayBuffer_featured as RB
     steps = int(os.environ.get("SP_STEPS", "20"))
-    mode = os.environ.get("SP_MODE", "plain")          # plain | gate | sleep
+    mode = os.environ.get("SP_MODE", "plain")          # plain | gate | sleep | syncs
     ug = {"auto": "auto", "1": True, "0": False}[os.environ.get("SP_GRAPH", "auto")]
     pol = TD3(Box((17,)), Box((6,)), max_action=1.0, device=0, seed=17, use_graph=ug)
     rb = RB(Box((17,)), Box((6,)), max_size=1_000_000, device=0, seed=101)
@@ -42,6 +42,27 @@ def main():
     stream = torch.cuda.ExternalStream(sp, device=0)
     hip, word = _gate(torch) if mode == "gate" else (None, None)
     per_call = [[], []]
+    if mode == "syncs":                                # what each way of ending a timed run costs
+        import numpy as np
+        forms = {"td3_sync + torch sync": lambda: (pol.sync(), torch.cuda.synchronize()),
+                 "torch sync only": lambda: torch.cuda.synchronize(),
+                 "td3_sync only": lambda: pol.sync(),
+                 "td3_sync + stream sync + torch sync": lambda: (pol.sync(), stream.synchronize(),
+                                                                 torch.cuda.synchronize()),
+                 "stream sync + torch sync": lambda: (stream.synchronize(), torch.cuda.synchronize())}
+        for name, fn in forms.items():
+            tt = []
+            for rep in range(12):
+                pol.sync()
+                torch.cuda.synchronize()
+                for i in range(steps):
+                    pol.train(rb, 256)
+                time.sleep(0.003)                      # the GPU is done: time the ending alone
+                a = time.perf_counter()
+                fn()
+                tt.append(time.perf_counter() - a)
+            print(f"syncs: {name:40s} median {1e6 * np.median(tt):6.1f} us  min {1e6 * min(tt):6.1f}", flush=True)
+        return
     for rep in range(8):
         pol.sync()
         torch.cuda.synchronize()
