@@ -529,11 +529,26 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
       const float z = wsum(part[o]) + b4v[o];
       if (c.lane == o) mine = z;
     }
-  for (int o = kHeadRegs; o < ad; ++o) {
-    float w[8];
-    rv_load(w, P.ex[3] + (size_t)o * ldw4, ldw4, c.lane);
-    const float z = wsum(rv_pdot(x[0], w, K3, c.lane)) + gld(P.ex[4] + o);
-    if (c.lane == o) mine = z;
+  // wide action spaces (Humanoid: 17): further blocks of kHeadRegs outputs, each block's W4 rows
+  // and biases requested in one batch (one load round trip per block; per output, the 9 extra
+  // Humanoid outputs were 9 dependent round trips: heads 8-9 us at B = 1024)
+  for (int ob = kHeadRegs; ob < ad; ob += kHeadRegs) {
+    float wb[kHeadRegs][8], bv[kHeadRegs];
+#pragma unroll
+    for (int o = 0; o < kHeadRegs; ++o) {
+      const int oo = ob + o < ad ? ob + o : 0;
+      rv_load(wb[o], P.ex[3] + (size_t)oo * ldw4, ldw4, c.lane);
+      bv[o] = gld(P.ex[4] + oo);
+    }
+    float pb[kHeadRegs];
+#pragma unroll
+    for (int o = 0; o < kHeadRegs; ++o) pb[o] = rv_pdot(x[0], wb[o], K3, c.lane);
+#pragma unroll
+    for (int o = 0; o < kHeadRegs; ++o)
+      if (ob + o < ad) {
+        const float z = wsum(pb[o]) + bv[o];
+        if (c.lane == ob + o) mine = z;
+      }
   }
   if (!target) {
     if (NORM) rv_store(P.ex[8] + (size_t)c.row * ld3, ld3, c.lane, x[0]);
