@@ -3237,19 +3237,31 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
 // on an interrupt once the wait grows long, and its wake-up added tens of us to the end of every
 // burst of steps (e.g. the 20-step timed runs of the driver's bench command).  One event record (a
 // marker packet) per call; the poll itself queues nothing.
+// The learner stream's work done.  Completion is detected by spinning on an event (a blocking
+// wait adds the runtime's wake-up latency), then the stream is synchronized as well: it has no
+// work left, so that call returns at once, but it lets the runtime retire the stream's launch
+// records, which a following device-wide sync (torch.cuda.synchronize) otherwise pays for.  On
+// an idle MI355X the pair td3_sync + torch.cuda.synchronize costs 42 us this way against 58 us
+// without the stream sync (tools/short_probe.py SP_MODE=syncs, round 4).  TD3_SYNC_MODE (A/B):
+// 0 event spin only, 1 event spin + stream sync (default), 2 stream sync only.
 int td3_sync(td3_handle* h) {
   TD3_ARG(h != nullptr, "null handle");
   TD3_HIP(hipSetDevice(h->cfg.device));
-  TD3_HIP(hipEventRecord(h->sync_ev, h->stream));
-  for (;;) {
-    const hipError_t e = hipEventQuery(h->sync_ev);
-    if (e == hipSuccess) return 0;
-    if (e != hipErrorNotReady) {
-      set_error("td3_sync: hipEventQuery: %s", hipGetErrorString(e));
-      return -2;
+  static const int mode = env_int("TD3_SYNC_MODE", 1);
+  if (mode != 2) {
+    TD3_HIP(hipEventRecord(h->sync_ev, h->stream));
+    for (;;) {
+      const hipError_t e = hipEventQuery(h->sync_ev);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) {
+        set_error("td3_sync: hipEventQuery: %s", hipGetErrorString(e));
+        return -2;
+      }
+      __builtin_ia32_pause();
     }
-    __builtin_ia32_pause();
   }
+  if (mode != 0) TD3_HIP(hipStreamSynchronize(h->stream));
+  return 0;
 }
 
 void* td3_stream(td3_handle* h) { return h ? (void*)h->stream : nullptr; }
