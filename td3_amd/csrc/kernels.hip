@@ -23,7 +23,6 @@
 // Compute dtype: fp32 everywhere.  Matrix products use v_mfma_f32_32x32x2_f32
 // (exact fp32 FMA chain, MI355X_MICROARCH.md § Matrix cores).
 #include <math.h>
-#include <stdlib.h>
 
 #include "dev.h"
 #include "kernels.h"
@@ -797,94 +796,6 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
   rv_store(P.ex[11] + (size_t)c.row * ld3, ld3, c.lane, gu3[0]);
   ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, NORM);        // dZ3 of the actor
   rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
-}
-
-// row_actor_head_bwd for wide action spaces at large batches (ad > kHeadRegs, B >= 512: Humanoid's
-// 17 outputs at B = 1024).  There every row re-reads the head's weights -- W1's action columns
-// (ad x K0) and W4 (ad x K3), 54 KB -- in one dependent load round trip per block of kHeadRegs
-// outputs, so a row's wave took 8 us (tools/tl_probe.py) and the stage 10.6 us.  Here the 4 waves
-// of a workgroup (4 rows) stage both weight blocks into LDS once, in one round trip beside their
-// rows, and every output block then reads LDS.  Same arithmetic in the same order as
-// row_actor_head_bwd (rv_load_lds returns the values rv_load would): bitwise equal.
-constexpr int kHeadLdsRows = 4;
-template <bool NORM>
-__global__ __launch_bounds__(64 * kHeadLdsRows) void actor_head_bwd_lds_kernel(int Bp, GemmTable tab) {
-  extern __shared__ float4 hl4[];
-  float* const hl = reinterpret_cast<float*>(hl4);
-  const GemmProb& P = tab.p[0];
-  asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.ex[3]), "s"(P.ex[4]), "s"(P.ex[5]),
-               "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.ex[11]),
-               "s"(P.ex[12]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]), "s"(P.exi[4]),
-               "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.exi[7]), "s"(P.exi[8]), "s"(P.exf[0]), "s"(P.Aout),
-               "s"(P.ldao), "s"(P.B));
-  const int K0 = P.exi[0], ld0 = P.exi[1], ad = P.exi[4];
-  const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7], ldt = P.exi[8];
-  const float ma = P.exf[0];
-  const int S1 = (K0 + 3) & ~3, S3 = (K3 + 3) & ~3;    // LDS row strides (launch_rows checks K0, K3 % 4)
-  float* const w1s = hl;                               // [ad][S1]: W1[:, sd + o] (the transposed copy)
-  float* const w4s = hl + ad * S1;                     // [ad][S3]: W4 rows
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row = blockIdx.x * kHeadLdsRows + wave;
-  // the row's operands first, then the weight blocks (all in flight together)
-  float gu0[1][8], h0[1][8], h3[1][8], g0[8], g3[8], mn0[1], rs0[1], mn3[1], rs3[1];
-  rv_load(gu0[0], P.ex[0] + (size_t)row * ld0, ld0, lane);
-  rv_load(h0[0], P.ex[1] + (size_t)row * ld0, ld0, lane);
-  rv_load(h3[0], P.ex[7] + (size_t)row * ld3, ld3, lane);
-  if (NORM) {
-    rv_load(g0, P.ex[3], ld0, lane);
-    rv_load(g3, P.ex[9], ld3, lane);
-    mn0[0] = gld(P.ex[2] + row);
-    rs0[0] = gld(P.ex[2] + (Bp + row));
-    mn3[0] = gld(P.ex[8] + row);
-    rs3[0] = gld(P.ex[8] + (Bp + row));
-  } else {
-    mn0[0] = mn3[0] = 0.f;
-    rs0[0] = rs3[0] = 1.f;
-  }
-  const float tl = lane < ad ? gld(P.ex[5] + ((size_t)row * 32 + lane)) : 0.f;
-  const int n1 = ad * (S1 >> 2), n3 = ad * (S3 >> 2);   // float4s per block
-  for (int e = threadIdx.x; e < n1 + n3; e += 64 * kHeadLdsRows) {
-    float4 v;
-    if (e < n1) {
-      const int o = e / (S1 >> 2), c = (e - o * (S1 >> 2)) * 4;
-      v = gld4(P.ex[12] + ((size_t)o * ldt + c));
-    } else {
-      const int f = e - n1, o = f / (S3 >> 2), c = (f - o * (S3 >> 2)) * 4;
-      v = gld4(P.ex[6] + ((size_t)o * ldw4 + c));
-    }
-    hl4[e] = v;
-  }
-  __syncthreads();
-  ln_bwd_rows<1>(gu0, h0, g0, mn0, rs0, K0, lane, NORM);       // dZ0 of Q1 (pads -> 0)
-  const bool live = row < P.B;
-  float gu3[1][8];
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) gu3[0][jj] = 0.f;
-  for (int ob = 0; ob < ad; ob += kHeadRegs) {
-    float w1b[kHeadRegs][8], w4b[kHeadRegs][8];
-#pragma unroll
-    for (int o = 0; o < kHeadRegs; ++o) {
-      const int oo = ob + o < ad ? ob + o : 0;
-      rv_load_lds(w1b[o], w1s + oo * S1, K0, lane);
-      rv_load_lds(w4b[o], w4s + oo * S3, ldw4 < S3 ? ldw4 : S3, lane);
-    }
-    float pb[kHeadRegs];
-#pragma unroll
-    for (int o = 0; o < kHeadRegs; ++o) pb[o] = rv_pdot(gu0[0], w1b[o], K0, lane);
-#pragma unroll
-    for (int o = 0; o < kHeadRegs; ++o)
-      if (ob + o < ad) {
-        const float ga = wsum(pb[o]);                                   // dL/da_o
-        const float t = __shfl(tl, ob + o, 64);
-        const float gz4 = live ? (ga * ma) * (1.f - t * t) : 0.f;       // max_action*tanh bwd
-        if (lane == 0) gst(P.ex[10] + ((size_t)row * 32 + ob + o), gz4);
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4b[o][jj];
-      }
-  }
-  rv_store(P.ex[11] + (size_t)row * ld3, ld3, lane, gu3[0]);
-  ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, lane, NORM);        // dZ3 of the actor
-  rv_store(P.Aout + (size_t)row * P.ldao, P.ldao, lane, gu3[0]);
 }
 
 // ================================================================== TD3_particles heads
@@ -3076,23 +2987,9 @@ static void launch_rows_t(int kind, const GemmTable& d, int Bp, hipStream_t s) {
     case kRowPolicyHead: hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
     case kRowCriticLoss: hipLaunchKernelGGL((row_kernel<kRowCriticLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
     case kRowActorLoss: hipLaunchKernelGGL((row_kernel<kRowActorLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
-    case kRowActorHeadBwd: {
-      // wide heads at large batches: the LDS-staged form (one weight round trip per 4 rows)
-      const char* env = getenv("TD3_HEAD_LDS");          // A/B switch (read per launch: tests flip it)
-      const bool lds_ok = !env || atoi(env) != 0;
-      const GemmProb& p = d.p[0];
-      const int ad = p.exi[4], K0 = p.exi[0], K3 = p.exi[5];
-      if (lds_ok && d.nprob == 1 && Bp >= 512 && Bp % kHeadLdsRows == 0 && ad > kHeadRegs && ad <= 32 &&
-          p.ex[12] && K0 % 4 == 0 && K3 % 4 == 0 && K0 <= 512 && K3 <= 512 && p.exi[7] >= K3 && p.exi[8] >= K0 &&
-          (size_t)ad * (K0 + K3) * sizeof(float) <= 65536) {
-        const size_t lds = (size_t)ad * (K0 + K3) * sizeof(float);
-        hipLaunchKernelGGL((actor_head_bwd_lds_kernel<NORM>), dim3(Bp / kHeadLdsRows), dim3(64 * kHeadLdsRows), lds, s,
-                           Bp, d);
-      } else {
-        hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
-      }
+    case kRowActorHeadBwd:
+      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
       break;
-    }
     case kRowCriticLossP:
       hipLaunchKernelGGL((row_kernel<kRowCriticLossP, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
       break;

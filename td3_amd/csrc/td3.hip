@@ -339,7 +339,6 @@ struct td3_handle {
   // last step that changed the online actor, so on critic-only steps (total_it % policy_freq != 0)
   // it overlaps the training step instead of queueing behind it.
   hipStream_t act_stream = nullptr;
-  hipEvent_t sync_ev = nullptr;               // td3_sync: the step stream's end, polled by the host
   hipEvent_t actor_ev = nullptr;              // recorded after every actor-updating step once a
                                               // query ran (act_used): an event record costs the
                                               // step's stream ~4 us, pure training needs none
@@ -2610,7 +2609,6 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   TD3_HIP(hipStreamCreateWithFlags(&h->act_stream, hipStreamNonBlocking));
   TD3_HIP(hipEventCreateWithFlags(&h->actor_ev, TD3_EV_FLAGS));
-  TD3_HIP(hipEventCreateWithFlags(&h->sync_ev, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -2643,7 +2641,6 @@ int td3_destroy(td3_handle* h) {
   (void)hipStreamSynchronize(h->act_stream);
   (void)hipStreamDestroy(h->act_stream);
   (void)hipEventDestroy(h->actor_ev);
-  (void)hipEventDestroy(h->sync_ev);
   (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -3237,30 +3234,14 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
 // on an interrupt once the wait grows long, and its wake-up added tens of us to the end of every
 // burst of steps (e.g. the 20-step timed runs of the driver's bench command).  One event record (a
 // marker packet) per call; the poll itself queues nothing.
-// The learner stream's work done.  Completion is detected by spinning on an event (a blocking
-// wait adds the runtime's wake-up latency), then the stream is synchronized as well: it has no
-// work left, so that call returns at once, but it lets the runtime retire the stream's launch
-// records, which a following device-wide sync (torch.cuda.synchronize) otherwise pays for.  On
-// an idle MI355X the pair td3_sync + torch.cuda.synchronize costs 42 us this way against 58 us
-// without the stream sync (tools/short_probe.py SP_MODE=syncs, round 4).  TD3_SYNC_MODE (A/B):
-// 0 event spin only, 1 event spin + stream sync (default), 2 stream sync only.
+// The learner stream's work done: hipStreamSynchronize.  Measured against spinning on an event
+// recorded on the stream (round 4, tools/short_probe.py, 20-step C2 runs): host time past the
+// GPU's own span 24-30 us per run against 35-38 us, and a following torch.cuda.synchronize()
+// 5-6 us against 21 us (the stream sync also lets the runtime retire the stream's launch records).
 int td3_sync(td3_handle* h) {
   TD3_ARG(h != nullptr, "null handle");
   TD3_HIP(hipSetDevice(h->cfg.device));
-  static const int mode = env_int("TD3_SYNC_MODE", 1);
-  if (mode != 2) {
-    TD3_HIP(hipEventRecord(h->sync_ev, h->stream));
-    for (;;) {
-      const hipError_t e = hipEventQuery(h->sync_ev);
-      if (e == hipSuccess) break;
-      if (e != hipErrorNotReady) {
-        set_error("td3_sync: hipEventQuery: %s", hipGetErrorString(e));
-        return -2;
-      }
-      __builtin_ia32_pause();
-    }
-  }
-  if (mode != 0) TD3_HIP(hipStreamSynchronize(h->stream));
+  TD3_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
 

@@ -406,26 +406,6 @@ def test_layer0_widths_teacher_forced(sd, ad):
         _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
 
 
-def test_wide_head_backward_lds_bitwise_equal(monkeypatch):
-    """Humanoid's 17-wide actor head at B = 1024 runs the LDS-staged head backward
-    (actor_head_bwd_lds_kernel); the per-row form (TD3_HEAD_LDS=0) must give the same bits:
-    two steps (critic and policy), actor parameters and Adam moments."""
-    S = featured_setup_dims(376, 17, 0.4, "layer", B=1024)
-    rs = np.random.RandomState(9)
-    draws = [(rs.randint(0, gen.BUFFER_ROWS, S["B"]), rs.standard_normal((S["B"], S["ad"])).astype(np.float32))
-             for _ in range(2)]
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("TD3_HEAD_LDS", flag)
-        pol, rb = _make(S, use_graph=False)
-        for idx, noise in draws:
-            pol.train_step(rb, S["B"], indices=idx, noise=noise)
-        outs.append((pol.actor.flat(), pol.actor_optimizer.state_dict()["state"][0]["exp_avg"].numpy(),
-                     pol.actor_optimizer.state_dict()["state"][5]["exp_avg_sq"].numpy()))
-    for a, b in zip(*outs):
-        np.testing.assert_array_equal(a, b)
-
-
 @pytest.mark.parametrize("B", [512, 1024])
 def test_large_batch_teacher_forced(B):
     """Batches >= 512 switch the wide stages to 128-column GEMM workgroups with the K chunks
