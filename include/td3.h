@@ -209,7 +209,9 @@ int td3_comm_unique_id(unsigned char out[128]);
 /* Data-parallel mode: grads are all-reduced (sum, then /world) over RCCL before Adam.  Every
  * call that steps the learner is then COLLECTIVE: td3_train_step / td3_train_step_batch and
  * td3_actor_learn_particles must be made by every rank in the same order (each issues the
- * phase all-reduces). */
+ * phase all-reduces).  With TD3_DP_BUCKETS=1 in the environment when the plan is built, a twin
+ * critic at B >= 512 exchanges its gradients per network, bucket 0 on a comm stream under
+ * bucket 1's dW (off by default: measured slower on one rank). */
 int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int rank);
 /* Test seam of the same data-parallel path inside ONE process (RCCL cannot put two ranks on one
  * GPU): the n handles (same configuration and device) become the ranks 0..n-1 of a group whose
@@ -224,6 +226,7 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
                          const float* inject_noise, td3_step_stats* stats);
 
 /* ------------------------------------------------------------------ measurement */
+/* Block until the learner stream's queued work is done (hipStreamSynchronize). */
 int td3_sync(td3_handle* h);
 void* td3_stream(td3_handle* h);
 /* Per-stage device times (ms) of one eager step; names via td3_stage_name. */
