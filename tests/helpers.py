@@ -76,3 +76,54 @@ def params_close(P, golden, prefix, salt_base, atol, rtol=1e-5, frac_loose=1e-3,
         bad = err > tol
         assert bad.mean() <= frac_loose or bad.sum() <= 1, (prefix, k, bad.sum(), err.max())
         assert err.max() <= loose, (prefix, k, err.max())
+
+
+def oracle_dp_step(L, batch, noise, n, step_fn=None):
+    """The oracle's restatement of the product's data-parallel step: n Learner copies
+    in lock-step (threads), replica k on rows [k*b, (k+1)*b) of the batch; each phase's gradients
+    summed over replicas in replica order (((g0 + g1) + g2) ..., as local_sum_kernel) and scaled by
+    float32(1/n) (adam_flat_kernel's grad_scale) before the oracle's own Adam + Polyak.  Returns
+    replica 0's Learner (all replicas end identical).  Against this, the GPU data-parallel step
+    differs only by the summation order inside each shard, as the single-device tests do."""
+    import copy
+    import threading
+    step_fn = step_fn or orc.featured_train_step
+    B = batch[0].shape[0]
+    b = B // n
+    Ls = [copy.deepcopy(L) for _ in range(n)]
+    bar = threading.Barrier(n)
+    slots = [None] * n
+    red = {}
+    errs = []
+
+    def hook_for(k):
+        def hook(grads):
+            slots[k] = grads
+            bar.wait()
+            if k == 0:
+                red.clear()
+                for name, g0 in slots[0].items():
+                    acc = np.asarray(g0, np.float32)
+                    for j in range(1, n):
+                        acc = (acc + np.asarray(slots[j][name], np.float32)).astype(np.float32)
+                    red[name] = (acc * np.float32(1.0 / n)).astype(np.float32)
+            bar.wait()
+            return {name: v.copy() for name, v in red.items()}
+        return hook
+
+    def run(k):
+        try:
+            shard = tuple(x[k * b:(k + 1) * b] for x in batch)
+            step_fn(Ls[k], shard, noise[k * b:(k + 1) * b], grad_hook=hook_for(k))
+        except Exception as e:                      # pragma: no cover - surfaced below
+            errs.append(e)
+            bar.abort()
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+    return Ls[0]
