@@ -25,9 +25,23 @@ def _gate(torch):
     return hip, word
 
 
+def _set_flags(when):
+    """SP_SPIN=pre|post[:flag]: hipSetDeviceFlags(flag) (1 spin, 2 yield, 4 blocking sync) before
+    the first HIP call or after torch made the device current."""
+    spec = os.environ.get("SP_SPIN", "")
+    if not spec.startswith(when):
+        return
+    flag = int(spec.split(":")[1]) if ":" in spec else 1
+    hip = C.CDLL("libamdhip64.so")
+    rc = hip.hipSetDeviceFlags(C.c_uint(flag))
+    print(f"hipSetDeviceFlags({flag}) {when} -> {rc}", flush=True)
+
+
 def main():
+    _set_flags("pre")
     import torch
     torch.cuda.set_device(0)
+    _set_flags("post")
     from td3_amd.TD3_featured import TD3
     from td3_amd.my_replay_buffer import ReplayBuffer_featured as RB
     steps = int(os.environ.get("SP_STEPS", "20"))
