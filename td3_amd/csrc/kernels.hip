@@ -1335,10 +1335,22 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
   const int s0 = cb + kCh;
   // WN = 4 (B >= 512, two workgroups per CU at <= 128 VGPRs) requests them after the prologue:
   // in flight during the LayerNorm they pushed the kernel past 128 VGPRs
+  // The fused layer-0 stages (kL0) request the first two streamed chunks right before the MFMA
+  // loop, unconditionally, the chunk index clamped to the wave's last chunk (a surplus load reads
+  // that chunk again and is never multiplied): behind a branch, the waitcnt pass could not count
+  // them and waited vmcnt(4) / vmcnt(0) before the first two chunks' MFMAs, i.e. for the chunks
+  // just requested (F_fwd01 ISA; C2 +1 %).  The other prologues issue them early (pro_ln) or
+  // measured slower unconditional (Humanoid MODE 1 stages: surplus strided loads).
+  const int clast = max(ce - 1, 0);
   auto issue_stream = [&]() {
     if constexpr (WN == 2) {
-      if (s0 < ce) load_chunk<MODE>(P, bs0, s0, ncol, h);
-      if (s0 + 1 < ce) load_chunk<MODE>(P, bs1, s0 + 1, ncol, h);
+      if constexpr (kL0) {
+        load_chunk<MODE>(P, bs0, min(s0, clast), ncol, h);
+        load_chunk<MODE>(P, bs1, min(s0 + 1, clast), ncol, h);
+      } else {
+        if (s0 < ce) load_chunk<MODE>(P, bs0, s0, ncol, h);
+        if (s0 + 1 < ce) load_chunk<MODE>(P, bs1, s0 + 1, ncol, h);
+      }
     }
   };
 
