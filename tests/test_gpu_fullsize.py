@@ -1,5 +1,6 @@
-"""Parity at BASELINE.json's full single-GPU configurations (SURVEY.md §8d C2 / C3).
+"""Parity at BASELINE.json's full single-GPU configurations (SURVEY.md §8d C1 / C2 / C3).
 
+* C1: Pendulum shapes (max_action 2.0), a ring of 1e5 rows, batch 256;
 * C2: HalfCheetah shapes, a ring of 1e6 rows, batch 256 -- the bench workload;
 * C3: Humanoid shapes, a ring of 2e6 rows (6.2 GB of 772-float records), batch 1024.
 
@@ -22,8 +23,9 @@ from test_gpu_parity import Box, _load_oracle_state, _params_close, _rel_to_max
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("sd,ad,ma,rows,B", [(17, 6, 1.0, 1_000_000, 256), (376, 17, 0.4, 2_000_000, 1024)],
-                         ids=["c2_halfcheetah", "c3_humanoid"])
+@pytest.mark.parametrize("sd,ad,ma,rows,B", [(3, 1, 2.0, 100_000, 256), (17, 6, 1.0, 1_000_000, 256),
+                                              (376, 17, 0.4, 2_000_000, 1024)],
+                         ids=["c1_pendulum", "c2_halfcheetah", "c3_humanoid"])
 def test_full_config_production_step(sd, ad, ma, rows, B):
     from td3_amd.TD3_featured import TD3
     from td3_amd.my_replay_buffer import ReplayBuffer_featured
