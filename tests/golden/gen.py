@@ -173,3 +173,26 @@ PARTICLE_CONFIGS = {
 
 BUFFER_ROWS = 1000
 SEED = 7
+
+# Long-horizon drift fixture (make_drift.py): HalfCheetah dims, LayerNorm, B = 256, 100 steps.
+DRIFT_CONFIG = (17, 6, 1.0, "layer", 256)       # sd, ad, max_action, norm, batch
+DRIFT_STEPS = 100
+DRIFT_SAMPLES = 64                              # exact values kept per tensor and step
+DRIFT_TARGET_EVERY = 10                         # target networks' samples every 10 steps
+
+
+def drift_draws(step, B, ad, size):
+    """The two RNG draws of ``train`` step `step` (indices of ``my_replay_buffer.py:120``, the
+    N(0,1) noise of ``TD3_featured.py:132``), deterministic so no fixture has to store them."""
+    rs = np.random.RandomState(10_000 + step)
+    idx = rs.randint(0, size, size=B).astype(np.int64)
+    noise = rs.standard_normal((B, ad)).astype(np.float32)
+    return idx, noise
+
+
+def summarize_k(arr, k, salt=0):
+    """``summarize`` with `k` sampled positions."""
+    a = np.asarray(arr, dtype=np.float32).reshape(-1)
+    pos = sample_positions(a.size, k=k, salt=salt)
+    a64 = a.astype(np.float64)
+    return np.array([a64.sum(), (a64 * a64).sum(), np.abs(a64).max()]), a[pos].copy()

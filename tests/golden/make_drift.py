@@ -1,0 +1,145 @@
+"""Long-horizon drift fixture: 100 free-running REFERENCE ``TD3.train`` steps.
+
+TEST INFRASTRUCTURE ONLY.  Run in the build container (where ``/root/reference``
+exists); the GPU box only reads the committed ``tests/golden/drift_hc_layer.npz``.
+
+The reference calls ``train`` once per env step for a whole run (``main.py:266-269``,
+``TD3_featured.py:123-171``).  Per-step parity (``make_golden.py``) covers 4 steps; this
+fixture pins the long horizon, with the contract of SURVEY.md §8c: free-running drift must
+stay within the reference's own fp32 drift, measured here as the reference against itself
+at 1 against 2, 4 and 8 torch threads (different summation orders, identical draws).
+
+1. Build ``TD3_featured.TD3`` at HalfCheetah dims (sd 17, ad 6, norm="layer") and load the
+   deterministic init of ``gen.init_params`` (online and target networks); fill the
+   reference buffer with ``gen.fill_featured_buffer`` through its own ``add``.
+2. Run ``DRIFT_STEPS`` steps of ``policy.train(rb, B)`` at 1 thread with the two RNG draws
+   inside ``train`` (``np.random.randint`` at ``my_replay_buffer.py:120``, ``torch.randn_like``
+   at ``TD3_featured.py:132``) replaced by ``gen.drift_draws(step)`` -- deterministic, so the
+   fixture stores no draws and the tests regenerate them.
+3. After every step store, per parameter tensor of actor / critic (and every
+   ``DRIFT_TARGET_EVERY`` steps actor_target / critic_target): the values at
+   ``gen.sample_positions(numel, DRIFT_SAMPLES)`` and (sum, sumsq, max|x|).
+4. Run the same steps at 2, 4 and 8 threads; per step and tensor store the max over those runs
+   of max |theta_1 - theta_t| over the whole tensor (``<group>/env``) and over the sampled
+   positions (``<group>/env_s``): the envelope of the reference's own fp32 realisations.  Arrays are [step, tensor] (tensor order ``<group>/names``, state_dict order).
+
+Usage:  python tests/golden/make_drift.py [--ref /root/reference]
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import gen  # noqa: E402
+from make_golden import _Box, _load  # noqa: E402
+
+GROUPS = ("actor", "critic", "actor_target", "critic_target")
+
+
+def run(ref_mods, torch, threads, record):
+    """DRIFT_STEPS reference steps at `threads`; `record(step, pol)` after each."""
+    TD3_featured, my_rb = ref_mods
+    sd, ad, ma, norm, B = gen.DRIFT_CONFIG
+    torch.set_num_threads(threads)
+    with contextlib.redirect_stdout(io.StringIO()):        # TD3_featured.py:103 prints params
+        pol = TD3_featured.TD3(_Box((sd,)), _Box((ad,)), max_action=ma, norm=norm)
+    a0 = gen.init_params(gen.featured_actor_shapes(sd, ad, norm), gen.SEED)
+    c0 = gen.init_params(gen.featured_critic_shapes(sd, ad, norm), gen.SEED + 100)
+    for m, p in ((pol.actor, a0), (pol.actor_target, a0), (pol.critic, c0), (pol.critic_target, c0)):
+        _load(m, p)
+    rb = my_rb.ReplayBuffer_featured(_Box((sd,)), _Box((ad,)), max_size=gen.BUFFER_ROWS)
+    s, a, s2, r, d = gen.fill_featured_buffer(sd, ad, ma, gen.BUFFER_ROWS, gen.SEED)
+    for i in range(gen.BUFFER_ROWS):
+        rb.add(s[i], a[i], s2[i], r[i], d[i])
+    orig_randint, orig_randn_like = np.random.randint, torch.randn_like
+    cur = {}
+
+    def randint(lo, hi=None, size=None, *a, **k):        # my_replay_buffer.py:120
+        assert lo == 0 and hi == rb.size and size == B, (lo, hi, size)
+        return cur["idx"].copy()
+
+    def randn_like(x, *a, **k):                           # TD3_featured.py:132
+        assert tuple(x.shape) == cur["noise"].shape
+        return torch.from_numpy(cur["noise"].copy())
+
+    np.random.randint, torch.randn_like = randint, randn_like
+    try:
+        for step in range(1, gen.DRIFT_STEPS + 1):
+            cur["idx"], cur["noise"] = gen.drift_draws(step, B, ad, rb.size)
+            pol.train(rb, B)
+            record(step, pol)
+    finally:
+        np.random.randint, torch.randn_like = orig_randint, orig_randn_like
+    return pol
+
+
+def _params(pol):
+    return {"actor": pol.actor, "critic": pol.critic, "actor_target": pol.actor_target,
+            "critic_target": pol.critic_target}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--threads", type=int, nargs="+", default=[2, 4, 8])
+    args = ap.parse_args()
+    sys.path.insert(0, args.ref)
+    import torch
+    import my_replay_buffer
+    import TD3_featured
+    mods = (TD3_featured, my_replay_buffer)
+
+    snaps = {}                                           # step -> group -> name -> full tensor
+
+    def keep(step, pol):
+        snaps[step] = {g: {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
+                       for g, m in _params(pol).items()}
+
+    run(mods, torch, 1, keep)
+    names = {g: list(snaps[1][g]) for g in GROUPS}
+    steps = np.arange(1, gen.DRIFT_STEPS + 1)
+    tsteps = np.array([s for s in steps if s % gen.DRIFT_TARGET_EVERY == 0 or s == gen.DRIFT_STEPS])
+    out = {"config/dims": np.array(list(gen.DRIFT_CONFIG[:2]) + [gen.DRIFT_CONFIG[4], gen.DRIFT_STEPS]),
+           "config/threads": np.array([1] + args.threads), "target_steps": tsteps}
+    for g in GROUPS:
+        out[f"{g}/names"] = np.array(names[g])
+        gs = tsteps if g.endswith("_target") else steps
+        st = np.zeros((len(gs), len(names[g]), 3))
+        smp = np.zeros((len(gs), len(names[g]), gen.DRIFT_SAMPLES), np.float32)
+        for a, s_ in enumerate(gs):
+            for i, k in enumerate(names[g]):
+                st[a, i], x = gen.summarize_k(snaps[s_][g][k], gen.DRIFT_SAMPLES, salt=i)
+                smp[a, i, :x.size] = x
+        out[f"{g}/stats"], out[f"{g}/samples"] = st, smp
+        out[f"{g}/env"] = np.zeros((len(steps), len(names[g])), np.float32)     # whole tensor
+        out[f"{g}/env_s"] = np.zeros((len(steps), len(names[g])), np.float32)   # sampled positions
+
+    def envelope(step, pol):
+        for g, m in _params(pol).items():
+            for i, (k, v) in enumerate(m.state_dict().items()):
+                a1 = snaps[step][g][k].reshape(-1)
+                a8 = v.detach().numpy().reshape(-1)
+                d = np.abs(a1.astype(np.float64) - a8)
+                pos = gen.sample_positions(a1.size, k=gen.DRIFT_SAMPLES, salt=i)
+                e, es = out[f"{g}/env"], out[f"{g}/env_s"]
+                e[step - 1, i] = max(e[step - 1, i], d.max())
+                es[step - 1, i] = max(es[step - 1, i], d[pos].max())
+
+    for t in args.threads:
+        run(mods, torch, t, envelope)
+    path = os.path.join(HERE, "drift_hc_layer.npz")
+    np.savez_compressed(path, **out)
+    env = np.max([out[f"{g}/env"].max(axis=1) for g in GROUPS], axis=0)
+    print("wrote", path, os.path.getsize(path), "bytes; envelope max|dtheta| at steps 1/10/50/100:",
+          env[0], env[9], env[49], env[-1])
+
+
+if __name__ == "__main__":
+    main()

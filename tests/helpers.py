@@ -127,3 +127,33 @@ def oracle_dp_step(L, batch, noise, n, step_fn=None):
     if errs:
         raise errs[0]
     return Ls[0]
+
+
+# ---------------------------------------------------------------- long-horizon drift
+DRIFT_FLOOR = 1e-7            # absolute floor: a few fp32 ulps of the O(0.1) parameters
+
+
+def drift_envelope(G):
+    """Per-step envelope of the reference's own fp32 drift (tests/golden/make_drift.py): the max
+    over every group and tensor of |theta_1thread - theta_t| (t = 2, 4, 8 threads, whole tensors),
+    as a running max over the steps so far."""
+    groups = ("actor", "critic", "actor_target", "critic_target")
+    env = np.max([G[f"{g}/env"].max(axis=1) for g in groups], axis=0)
+    return np.maximum.accumulate(env.astype(np.float64))
+
+
+def drift_check(G, step, group, params, env):
+    """max |theta - theta_ref| over the fixture's sampled positions of every tensor of `group`
+    at `step`, and that value over the envelope (the contract is ratio <= 1)."""
+    names = list(G[f"{group}/names"])
+    assert names == list(params), (group, names[:3], list(params)[:3])
+    if group.endswith("_target"):
+        row = int(np.nonzero(G["target_steps"] == step)[0][0])
+    else:
+        row = step - 1
+    worst = 0.0
+    for i, k in enumerate(names):
+        _, smp = gen.summarize_k(params[k], gen.DRIFT_SAMPLES, salt=i)
+        ref = G[f"{group}/samples"][row, i, :smp.size]
+        worst = max(worst, float(np.abs(smp.astype(np.float64) - ref).max()))
+    return worst, worst / (env[step - 1] + DRIFT_FLOOR)
