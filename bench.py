@@ -544,6 +544,9 @@ def result_line(args, cfg, world, dt, runs, roof=None, gat=None, rows=None, cpu=
                    "parallelism": f"dp{world}" if world > 1 else ("dp1-self" if args.dp_self else "single"),
                    "launch": args.launch, "norm": args.norm},
         "samples_per_s": round(steps_s * B * world, 1),
+        # the same rate counted per rank-gradient: every rank computes one batch-B gradient per step
+        # (N-GPU lines stay comparable with the per-GPU "@ batch 256" label)
+        "batch_gradients_per_s": round(steps_s * world, 3),
         "runs": [round(args.steps / r, 3) for r in runs],
         "value_is": f"median of {len(runs)} timed runs of {args.steps} steps each; one step = one "
                     f"optimizer step of every rank on a global batch of {B}x{world} rows",

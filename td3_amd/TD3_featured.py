@@ -112,6 +112,8 @@ class _AdamView:
 
     def state_dict(self):
         torch = _torch()
+        if getattr(self._o, "_dp_rccl", False):     # sharded moments: a collective gather first
+            check(self._o._lib.td3_dp_gather_optimizer_state(self._o._h), "td3_dp_gather_optimizer_state")
         m = _ParamView(self._o, self._m, self._group).numpy_dict()
         v = _ParamView(self._o, self._v, self._group).numpy_dict()
         step = self._step()

@@ -87,6 +87,7 @@ SIGNATURES = {
     "td3_comm_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
     "td3_comm_init": (C.c_int, [_P, C.POINTER(C.c_ubyte), C.c_int, C.c_int]),
     "td3_comm_init_local": (C.c_int, [C.POINTER(_P), C.c_int]),
+    "td3_dp_gather_optimizer_state": (C.c_int, [_P]),
     "td3_train_step_local": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int, _I64, _F,
                                        C.POINTER(td3_step_stats)]),
     "td3_sync": (C.c_int, [_P]),

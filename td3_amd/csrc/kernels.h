@@ -181,6 +181,20 @@ struct Gemv01Args {
 };
 int launch_gemv01(const Gemv01Args& a, int nprob, hipStream_t s);
 
+// The whole query in ONE launch (act_kernel): layers 0-1 as gemv01, layer 2 after an in-launch
+// hand-off of H1 (per-network counters), the head in the last-arriving workgroup.  Layer-2 columns
+// ride on the layer-1 column groups (N2 <= N1); X of l2 is l1's Y, H3 of the head is l2's Y.
+struct ActArgs {
+  Gemv01Args g;                         // layer 0 + layer 1 (g.l1.B = live rows)
+  GemvProb l2[2];                       // layer 2 per network
+  HeadProb head[2];                     // LN2 + head per network
+  int* ctr;                             // [network][2] hand-off counters, zero between launches
+  float max_action;
+  unsigned* flag;                       // nullable: [network] = seq once its outputs are written
+  unsigned seq;                         //   (mapped host memory: the host polls it, no stream sync)
+};
+int launch_act(const ActArgs& a, int nprob, hipStream_t s);
+
 // dZ = relu'(LN_bwd(dU)) on full rows (layer 0, where no GEMM follows).
 struct LnBwdProb {
   const float* GU; const float* H; const float* stats; const float* lng; int ld, K;
@@ -262,6 +276,11 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s);
 constexpr int kBumpActorOnly = 2;
 int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds_bytes,
                 Counters* bump, int bump_actor, hipStream_t s);
+// The fused layer-0 stages (kProL0 / kProL0G, same GemmProb contract) on 16-row tiles: 16 x 16*nct
+// layer-1 outputs per workgroup of nct * wk waves; instantiated (nct, wk) = (5, 2), (2, 4).
+int launch_l0r16(int nct, int wk, int gather, const GemmTable& t, int nblocks, int Bp, Counters* bump,
+                 int bump_actor, hipStream_t s);
+int l0r16_lds_bytes(int Kp, int nct, int wk);
 // Two independent GEMM stages in one launch (stage 2's tile ids follow stage 1's); only the pairs
 // gemm2_supported() reports are instantiated.
 int gemm2_supported(int m1, int w1, int p1, int m2, int w2, int p2);

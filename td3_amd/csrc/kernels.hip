@@ -34,10 +34,14 @@ namespace td3 {
 // loop / after its own stores drained, plus the XCC id.  Read back with td3_tl_read.
 #ifdef TD3_TL
 __device__ unsigned long long td3_tl[8192][8];
+// shader-clock counter (s_memtime) beside the 100 MHz marks 1 and 2 (prologue barrier, end of the
+// MFMA loop): (clk[1] - clk[0]) / (tl[2] - tl[1]) * 100 MHz = the clock the MFMA phase ran at
+__device__ unsigned long long td3_clk[8192][2];
 __device__ __forceinline__ void tl_mark(int k) {
   const unsigned id = blockIdx.x + blockIdx.y * gridDim.x;
   if (threadIdx.x == 0 && id < 8192) {
     if (k == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (k == 1 || k == 2) td3_clk[id][k - 1] = __builtin_amdgcn_s_memtime();
     td3_tl[id][k] = __builtin_amdgcn_s_memrealtime();
     if (k == 0) {
       unsigned x, hw;
@@ -48,14 +52,46 @@ __device__ __forceinline__ void tl_mark(int k) {
   }
 }
 #define TL_MARK(k) tl_mark(k)
+// every GEMM workgroup's MFMA phase (prologue barrier -> end of the MFMA loop) summed over launches:
+// [0] shader-clock ticks (s_memtime), [1] 100 MHz ticks (s_memrealtime); read / cleared with
+// td3_clk_sum_read (tools/clk_probe.py: the clock a run's MFMA phases ran at)
+__device__ unsigned long long td3_clk_sum[2];
+#define TL_CLK_BEGIN() const unsigned long long tl_c0 = __builtin_amdgcn_s_memtime(), tl_r0 = __builtin_amdgcn_s_memrealtime()
+#define TL_CLK_END()                                                                             \
+  do {                                                                                         \
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0) {                                                                    \
+      atomicAdd(&td3_clk_sum[0], c1 - tl_c0);                                                  \
+      atomicAdd(&td3_clk_sum[1], r1 - tl_r0);                                                  \
+    }                                                                                          \
+  } while (0)
 #else
 #define TL_MARK(k)
+#define TL_CLK_BEGIN()
+#define TL_CLK_END()
 #endif
 #ifdef TD3_TL_FINE      // drain the loads at the mark (changes the overlap: phase attribution only)
 #define TL_FINE(k) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); TL_MARK(k); } while (0)
 #else
 #define TL_FINE(k)
 #endif
+
+// A workgroup barrier for LDS hand-offs only: this wave's LDS accesses complete, then s_barrier.
+// __syncthreads() is a workgroup-scope release + acquire, which on gfx950 waits vmcnt(0): every
+// load the wave has in flight (the streamed weights) drains at each prologue barrier.  The asm's
+// memory clobber keeps the compiler from moving LDS accesses across it; global memory needs no
+// ordering at these barriers (no workgroup reads global data another of its waves stored).
+// TD3_SYNC_BARRIERS=1 restores __syncthreads() (A/B builds).
+#ifndef TD3_SYNC_BARRIERS
+#define TD3_SYNC_BARRIERS 0
+#endif
+__device__ __forceinline__ void lds_barrier() {
+#if TD3_SYNC_BARRIERS
+  __syncthreads();
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
 
 __device__ __forceinline__ void lds_put_row(float* smem, int S, int row, int Kp, int lane, const float (&v)[8]) {
   lds_store8(smem + row * S, Kp, lane, v);
@@ -1367,18 +1403,19 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
       else load_b<MODE, kCh>(P, bv, cb, nch, ncol, h);
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
+    lds_barrier();
     TL_MARK(6);
     l0_mfma(P, xs, smem, xs + 32 * kL0XS, c, w0, b0v);
     if (P.norm) {
-      __syncthreads();
+      lds_barrier();
       TL_MARK(7);
       l0_ln(P, smem, c, lg, lb);
     }
     issue_stream();
   }
-  __syncthreads();
+  lds_barrier();
   TL_MARK(1);
+  TL_CLK_BEGIN();
   if constexpr (PRO != kProLN && !kL0) issue_stream();
   if constexpr (wn_cols(WN) == 4) {
     if (s0 < ce) load_chunk<MODE>(P, bs0, s0, ncol, h);
@@ -1454,6 +1491,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
     }
   }
 
+  TL_CLK_END();
   if constexpr (kL0) l0_store_rows<NT>(P, smem, smem + 32 * S + 32 * kL0XS, c);
   if constexpr (WK == 1 && WN != 0) {
     if (active) {
@@ -1474,7 +1512,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
     float* red = smem;  // [NW][32][33]; wave = wk * WNS + wn; one row tile at a time
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      __syncthreads();
+      lds_barrier();
       if constexpr (WN == 0) {
         // 16x16 C/D map: column lane & 15, row 4 * (lane >> 4) + j
 #pragma unroll
@@ -1486,7 +1524,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
 #pragma unroll
         for (int r = 0; r < 16; ++r) red[(wave * 32 + mfma_row(r, lane)) * 33 + i] = acc[rt][r];
       }
-      __syncthreads();
+      lds_barrier();
       TL_MARK(2);
       // (32 x OUTW outputs over NT threads: 16 waves of a 16-column tile leave half the threads idle)
 #pragma unroll
@@ -1574,6 +1612,272 @@ __global__ __launch_bounds__(64 * kNW, (W1 == 4 || W2 == 4) ? 4 : (W1 == kWn4x2 
     const int l = id - 8 * per1, b = (l & 7) * per2 + (l >> 3);
     if (b >= nb2) return;
     gemm_body<M2, W2, P2>(b, np2, c1, c2, c3, Bp, t2, nullptr, 0, smem);
+  }
+}
+
+// ================================================================== 16-row fused layer 0-1
+// The fused layer-0 stages (kProL0 / kProL0G: F_fwd01 with the step's sample, AF_fwd01) on 16-row
+// tiles (VERDICT r04 #1a).  A 32-row workgroup spends most of its span on row-serial work before its
+// first layer-1 MFMA (F_fwd01, profiles/r04_timeline_halfcheetah.txt: 8.4 of 14.9 us = records,
+// layer 0 over 512 columns, LayerNorm 0); half the rows halve the layer-0 MFMAs and the LayerNorm
+// rows per wave, and the 16 x 16*NCT output tile (v_mfma_f32_16x16x4_f32) halves the layer-1 chain
+// of a 32 x 64 tile at NCT = 4.  Workgroup = NW = NCT * WK waves (8 .. 16), tile (16 rows, 16*NCT
+// layer-1 columns) of one network; the problem directory, XCD-aware tile order and every output
+// (H1, H0 / U0 slices, LN0 statistics, the sample's copies, reward / not_done, drawn rows) are
+// gemm_body's kProL0 / kProL0G contract (kernels.h), so the planner swaps the launch only.
+//  1. input rows: thread t (< 512) stages x[t / 32][t % 32] (kProL0G: the Philox row drawn per
+//     thread, the record read unconditionally and masked at the LDS put), then W0 / b0 / LN0 affine
+//     requests; kProL0G requests the layer-1 weights after the records landed (TD3_L0G_LATE_B),
+//  2. layer 0: 16 x 16 tiles tau = wave + NW*q of Z0 = X W0^T on v_mfma_f32_16x16x4_f32, min(K0, 8)
+//     MFMAs per tile (lane group g supplies k = 8g + s), + b0, ReLU into the A buffer,
+//  3. LayerNorm 0 in place (rows w and w + NW of wave w),
+//  4. layer 1: wave (c = w % NCT, kq = w / NCT): 16 x 16 columns 16c.., K range kq of WK, chunks of
+//     32 (lane group g: k = kb + 8g + s, 2 ds_read_b128 per row chunk), partials summed through LDS.
+constexpr int kR16XS = 36;      // LDS row stride of the staged 16 input rows
+
+template <int NCT, int WK, bool GATHER>
+__global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
+                                                              GemmTable tab, Counters* bump, int bump_actor) {
+  constexpr int NW = NCT * WK, NT = 64 * NW, OUTW = 16 * NCT;
+  static_assert(NW >= 8 && NW <= 16 && NT % OUTW == 0, "l0r16: 8 .. 16 waves, whole output rows per pass");
+  extern __shared__ float4 smem4[];
+  float* smem = reinterpret_cast<float*>(smem4);
+  const int b = xcd_tile(nb);
+  TL_MARK(0);
+  if (b >= nb) return;
+  int pi = 0;
+  if (nprob > 1 && b >= tb1) pi = 1;
+  if (nprob > 2 && b >= tb2) pi = 2;
+  if (nprob > 3 && b >= tb3) pi = 3;
+  pi = __builtin_amdgcn_readfirstlane(pi);
+  const GemmProb& P = tab.p[pi];
+  if constexpr (GATHER)
+    asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
+                 "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
+                 "s"(P.norm), "s"(P.B), "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.seed),
+                 "s"(tab.rs.ctr), "s"(P.exi[0]), "s"(P.exi[1]));
+  else
+    asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
+                 "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
+                 "s"(P.norm), "s"(P.B));
+  const int mtiles = Bp >> 4;
+  const int t = b - P.tile_begin;
+  const int mt = t % mtiles, nt = t / mtiles;
+  const int m0 = mt * 16, n0 = nt * OUTW;
+  const int Kp = P.Kp;                          // layer-1 K = layer-0 padded width (<= 512)
+  const int S = lds_stride(Kp);
+  float* abuf = smem;                           // [16][S]: H0, then U0 = LN0(H0): layer 1's A rows
+  float* xs = abuf + 16 * S;                    // [16][kR16XS]: the input rows
+  float* h0s = xs + 16 * kR16XS;                // [16][S]: H0 kept for its store when LN0 overwrites abuf
+  float* red = h0s + 16 * S;                    // [NW][16][17]: layer-1 K-split partials
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j16 = lane & 15, g = lane >> 4;
+  const int K0 = P.exi[6], N0p = P.exi[5];
+  const bool t0 = nt == 0;
+  // ---- 1. input rows (loads first: the record reads are the latency-critical ones)
+  const int xrow = (threadIdx.x >> 5) & 15, xcol = threadIdx.x & 31;
+  const bool xown = threadIdx.x < 512;
+  const int grow_x = m0 + xrow;
+  int64_t idx = 0;
+  float xv, rw = 0.f;
+  if constexpr (GATHER) {
+    const uint64_t step = (uint64_t)(tab.rs.ctr->total_it + 1);
+    const uint64_t n = (uint64_t)*tab.rs.d_size;
+    idx = grow_x < P.B ? (int64_t)philox_index(tab.rs.seed, step, (uint32_t)grow_x, n) : -1;
+    __builtin_amdgcn_sched_barrier(0);
+    const float* rec = tab.rs.data + (size_t)(idx >= 0 ? idx : 0) * tab.rs.rec;
+    xv = gld(rec + P.exi[0] + (xcol < K0 ? xcol : 0));
+    rw = t0 ? gld(rec + P.exi[1] + (xcol & 1)) : 0.f;
+  } else {
+    xv = gld(P.A + (size_t)grow_x * P.lda + xcol);   // input rows are >= 32 wide (zero pads)
+  }
+  // layer-0 weights of this wave's tiles (B operand: W0[tau*16 + j16][8g + s], two float4 per tile:
+  // element-wise loads at k = KS*g + s were 16 scattered lines per instruction and held the record
+  // reads' landing ~3 us behind the 32-row kernel's) and biases.  MFMA s covers k = 8g + s, g = 0..3
+  // (x and W0 pads past K0 are zero): MFMAs s >= K0 read only pads and are skipped
+  const int n0t = N0p >> 4;                     // layer-0 column tiles of 16
+  constexpr int kQ0 = (32 + NW - 1) / NW;       // tiles per wave (N0p <= 512)
+  float w0[kQ0][8], b0v[kQ0];
+#pragma unroll
+  for (int q = 0; q < kQ0; ++q) {
+    const int tau = min(wave + NW * q, n0t - 1);
+    const float* wp = P.ex[8] + (size_t)(tau * 16 + j16) * 32 + 8 * g;
+    const float4 u = gld4(wp), v = gld4(wp + 4);
+    w0[q][0] = u.x; w0[q][1] = u.y; w0[q][2] = u.z; w0[q][3] = u.w;
+    w0[q][4] = v.x; w0[q][5] = v.y; w0[q][6] = v.z; w0[q][7] = v.w;
+    b0v[q] = gld(P.ex[9] + tau * 16 + j16);
+  }
+  float lg[8], lb[8];
+  if (P.norm) {
+    rv_load(lg, P.lng, Kp, lane);
+    rv_load(lb, P.lnb, Kp, lane);
+  }
+  // layer-1 weights: wave (c, kq) streams W1[n0 + 16c + j16][k] over its K range in 32-deep chunks
+  const int c = wave % NCT, kq = wave / NCT;
+  const int nch = Kp >> 5;
+  const int cb = kq * nch / WK, ce = (kq + 1) * nch / WK;
+  constexpr int kMaxCh = (16 + WK - 1) / WK;    // chunks of a wave at Kp = 512
+  const int ncol = n0 + 16 * c + j16;
+  const bool cact = n0 + 16 * c < P.Nout;
+  const int wrow = cact ? ncol : 0;
+  float bw[kMaxCh][8];
+  auto load_w1 = [&]() {
+#pragma unroll
+    for (int q = 0; q < kMaxCh; ++q) {
+      const int ch = min(cb + q, ce - 1);
+      const float* wp = P.W + (size_t)wrow * P.ldw + ch * 32 + 8 * g;
+      const float4 u = gld4(wp), v = gld4(wp + 4);
+      bw[q][0] = u.x; bw[q][1] = u.y; bw[q][2] = u.z; bw[q][3] = u.w;
+      bw[q][4] = v.x; bw[q][5] = v.y; bw[q][6] = v.z; bw[q][7] = v.w;
+    }
+  };
+  constexpr bool kLateB = GATHER && TD3_L0G_LATE_B;
+  if constexpr (!kLateB) load_w1();
+  const int ocol = threadIdx.x % OUTW;          // the epilogue's column (NT % OUTW == 0)
+  const float bias = P.bias && n0 + ocol < P.Nout ? gld(P.bias + n0 + ocol) : 0.f;
+  TL_MARK(5);
+  // put the input rows; n-tile 0 stores the sample's copies / reward / not_done / drawn rows
+  if (xown) {
+    const bool valid = xcol < K0;
+    const float x = (!GATHER || (idx >= 0 && valid)) ? xv : 0.f;
+    xs[xrow * kR16XS + xcol] = x;
+    if constexpr (GATHER) {
+      if (t0) {
+        if (valid) {
+          if (P.ex[3]) gst(P.ex[3] + (size_t)grow_x * P.exi[8] + xcol, x);
+          if (P.ex[0]) gst(P.ex[0] + (size_t)grow_x * P.exi[3] + xcol, x);
+        }
+        if (xcol < 2 && rw_ptr(P, xcol)) gst(rw_ptr(P, xcol) + grow_x, idx >= 0 ? rw : 0.f);
+        if (pi == 0 && tab.rs.idx_out && xcol == 0 && grow_x < P.B) tab.rs.idx_out[grow_x] = idx;
+      }
+    }
+  }
+  lds_barrier();
+  TL_MARK(6);
+  // kProL0G: the layer-1 weights (160 KB per workgroup at 80 columns) are requested only now, behind
+  // the staged rows: issued before the put, they shared the CU's ~70 GB/s L2 rate with the records
+  // and W0 and the put landed ~2.7 us later (tools/tl_probe.py); they are not needed before the
+  // LayerNorm, and the LDS-only barriers do not drain them
+  if constexpr (kLateB) {
+    load_w1();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // ---- 2. layer 0 on MFMA: A = the staged rows (lane (j16, g) supplies x[j16][8g + s])
+  const bool keep = P.ex[10] && P.norm;
+  {
+    const float4 x0 = *reinterpret_cast<const float4*>(xs + j16 * kR16XS + 8 * g);
+    const float4 x1 = *reinterpret_cast<const float4*>(xs + j16 * kR16XS + 8 * g + 4);
+    const float av[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    const int ks = min(K0, 8);                  // MFMA s reads k = 8g + s: all past K0 when s >= K0
+    f32x4 acc0[kQ0];
+#pragma unroll
+    for (int q = 0; q < kQ0; ++q) {
+      acc0[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (wave + NW * q >= n0t) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2)
+        if (s2 < ks) acc0[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w0[q][s2], acc0[q], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < kQ0; ++q) {
+      const int tau = wave + NW * q;
+      if (tau >= n0t) continue;
+      const int col = tau * 16 + j16;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float h = fmaxf(acc0[q][v] + b0v[q], 0.f);
+        abuf[(4 * g + v) * S + col] = h;
+        if (keep) h0s[(4 * g + v) * S + col] = h;
+      }
+    }
+  }
+  // ---- 3. LayerNorm 0 in place (wave w: rows w and w + NW)
+  if (P.norm) {
+    lds_barrier();
+    TL_MARK(7);
+    const int r0 = wave, r1 = wave + NW < 16 ? wave + NW : wave;
+    float x[2][8], mean[2], rstd[2], rm[8];
+    rv_load_lds(x[0], abuf + r0 * S, Kp, lane);
+    rv_load_lds(x[1], abuf + r1 * S, Kp, lane);
+    real_mask(rm, P.Kreal, lane);
+    ln_fwd_rows_pk<2>(x, lg, lb, rm, 1.0f / (float)P.Kreal, mean, rstd);
+    lds_store8(abuf + r0 * S, Kp, lane, x[0]);
+    if (wave + NW < 16) lds_store8(abuf + r1 * S, Kp, lane, x[1]);
+    if (t0 && P.stats && lane == 0) {
+      gst(P.stats + (m0 + r0), mean[0]);
+      gst(P.stats + (Bp + m0 + r0), rstd[0]);
+      if (wave + NW < 16) {
+        gst(P.stats + (m0 + r1), mean[1]);
+        gst(P.stats + (Bp + m0 + r1), rstd[1]);
+      }
+    }
+  }
+  lds_barrier();
+  TL_MARK(1);
+  TL_CLK_BEGIN();
+  // ---- 4. layer 1: 16 x 16 output of column tile c over chunks [cb, ce)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (cact) {
+    const float* ar = abuf + j16 * S + 8 * g;
+#pragma unroll
+    for (int q = 0; q < kMaxCh; ++q) {
+      if (cb + q < ce) {
+        const int kb = (cb + q) * 32;
+        const float4 u = *reinterpret_cast<const float4*>(ar + kb);
+        const float4 v = *reinterpret_cast<const float4*>(ar + kb + 4);
+        const float a8[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a8[s2], bw[q][s2], acc, 0, 0, 0);
+      }
+    }
+  }
+  TL_CLK_END();
+  // H0 / U0 rows of the tile, each n-tile workgroup its slice of the columns (after the MFMA loop:
+  // in the prologue they queued ahead of the weight stream)
+  {
+    float* H0 = P.ex[10];
+    float* U0 = P.norm ? P.Aout : nullptr;
+    const float* hsrc = P.norm ? h0s : abuf;
+    if (H0 || U0) {
+      const int nq = Kp >> 2;
+      const int q0 = nt * nq / P.ntiles, per = (nt + 1) * nq / P.ntiles - q0;
+      for (int e = threadIdx.x; e < 16 * per; e += NT) {
+        const int row = e / per, q4 = 4 * (q0 + e % per);
+        const size_t grow = (size_t)(m0 + row);
+        if (H0) gst4(H0 + grow * P.exi[5] + q4, *reinterpret_cast<const float4*>(hsrc + row * S + q4));
+        if (U0) gst4(U0 + grow * P.ldao + q4, *reinterpret_cast<const float4*>(abuf + row * S + q4));
+      }
+    }
+  }
+  // K-split partials through LDS (16 x 16 C map: column j16, rows 4g + v), bias, ReLU, store
+#pragma unroll
+  for (int v = 0; v < 4; ++v) red[(wave * 16 + 4 * g + v) * 17 + j16] = acc[v];
+  lds_barrier();
+  TL_MARK(2);
+#pragma unroll
+  for (int e0 = 0; e0 < 16 * OUTW; e0 += NT) {
+    const int e = e0 + threadIdx.x;
+    const int row = e / OUTW, cc = ocol >> 4, jj = ocol & 15;
+    float v = red[((0 * NCT + cc) * 16 + row) * 17 + jj];
+#pragma unroll
+    for (int w = 1; w < WK; ++w) v = v + red[((w * NCT + cc) * 16 + row) * 17 + jj];
+    if (P.bias) v = v + bias;
+    if (P.relu) v = fmaxf(v, 0.f);
+    if (n0 + ocol < P.Nout) gst(P.C + ((size_t)(m0 + row) * P.ldc + n0 + ocol), v);
+  }
+  TL_MARK(3);
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bump_actor != kBumpActorOnly) {
+      bump->total_it += 1;
+      bump->critic_step += 1;
+      bump->pw[0] *= bump->beta[0];
+      bump->pw[1] *= bump->beta[1];
+    }
+    if (bump_actor) {
+      bump->actor_step += 1;
+      bump->pw[2] *= bump->beta[2];
+      bump->pw[3] *= bump->beta[3];
+    }
   }
 }
 
@@ -1718,6 +2022,234 @@ __global__ __launch_bounds__(256) void gemv01_kernel(Gemv01Args a) {
         if (jj == j && rr == r) v = z[jj][rr];
     gst(P.Y + (size_t)r * P.ldy + o0 + j, fmaxf(v + gld(P.b + o0 + j), 0.f));
   }
+}
+
+// ================================================================== one-launch query (select_action)
+// select_action / eval_q of n <= kGemvRows rows as ONE launch (TD3_featured.py:113-121; VERDICT
+// r04 #6).  Grid (nb, networks) of 256-thread workgroups; workgroup b of network k:
+//   1. requests its layer-1 and layer-2 weight rows (4 + 4 per wave: nothing in the launch writes
+//      them), computes all of H0 = relu(W0 x + b0) into LDS (the query is in the arguments),
+//   2. layer 1, columns 16b .. 16b+15 (LN0 in the prologue), stored write-through (sc1),
+//   3. hands off: every storing wave drains its stores, the workgroup meets at a barrier, one lane
+//      adds to the network's layer-1 counter; one lane polls it (sc1 loads) up to nb arrivals,
+//   4. layer 2, the same 16 columns, from the H1 rows read with sc1 loads (LN1), stored sc1,
+//   5. arrives on the network's second counter; the LAST arriver (the value its add returned) reads
+//      H2 with sc1 loads, applies LN2 and the head, writes the outputs and zeroes both counters
+//      (every workgroup has passed its layer-1 poll before its second add).
+// The hand-off is MI355X_MICROARCH.md's sc1 form (stores and loads of the handed-off rows all sc1,
+// each storing wave's vmcnt(0) before the workgroup barrier, one agent-scope atomic per workgroup).
+// A poll that sees no progress for ~2^22 rounds gives up and the outputs are NaN (no hang).
+__device__ __forceinline__ float ald(const float* p) {
+  return __hip_atomic_load((const GAS float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ast(float* p, float v) {
+  __hip_atomic_store((GAS float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void rv_load_sc1(float (&v)[8], const float* row, int n, int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = rcol(lane, j);
+    v[j] = c < n ? ald(row + c) : 0.f;
+  }
+}
+
+template <int R, int KQ>    // KQ: float4 steps of a layer-0 row (K0 <= 4 * KQ)
+__global__ __launch_bounds__(256) void act_kernel(ActArgs a) {
+  __shared__ float h0[R][512];
+  __shared__ int s_flag;
+  TL_MARK(0);
+  const int k = blockIdx.y;
+  const GemvProb& P1 = a.g.l1.p[k];
+  const GemvProb& P2 = a.l2[k];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int B = a.g.l1.B;
+  const int o0 = (blockIdx.x * 4 + wave) * 4;            // this wave's 4 columns of layers 1 and 2
+  int* c1 = a.ctr + 2 * k;
+  int* c2 = c1 + 1;
+  // layer 0's weights first (H0 waits for them alone: vmcnt retires in order), coalesced: thread t
+  // holds columns 4*kg .. 4*kg + 3 (kg = t % TPR) of rows rsub + RPP*i, a wave's loads whole
+  // contiguous rows (one row per thread was a 64-line scatter per load: ~2 us of H0, act_tl.py)
+  const float* W0 = a.g.W0[k];
+  const float* b0 = a.g.b0[k];
+  constexpr int LW = 4 * KQ;                  // W0 row stride (floats): 32 or 64
+  constexpr int TPR = LW / 4, RPP = 256 / TPR, NPASS = 512 / RPP;
+  const int kg = threadIdx.x % TPR, rsub = threadIdx.x / TPR;
+  float4 w0r[NPASS];
+  float b0r[NPASS];
+#pragma unroll
+  for (int i = 0; i < NPASS; ++i) {           // unconditional (rows past N0 clamp; pads are zero)
+    const int o = min(rsub + RPP * i, a.g.N0 - 1);
+    w0r[i] = gld4(W0 + (size_t)o * LW + 4 * kg);
+    b0r[i] = gld(b0 + o);
+  }
+  float xr[R][4];                             // the query values of this thread's 4 columns (xq is
+#pragma unroll                                // zero past B*K0; past K0 the weights are zero)
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) xr[r][jj] = a.g.xq[min(r * a.g.K0 + 4 * kg + jj, kGemvQ - 1)];
+  float w1[4][8], w2[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rv_load(w1[j], P1.W + (size_t)min(o0 + j, P1.N - 1) * P1.ldw, P1.K, lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rv_load(w2[j], P2.W + (size_t)min(o0 + j, P2.N - 1) * P2.ldw, P2.K, lane);
+  float g1[8], bb1[8], g2[8], bb2[8], rm1[8], rm2[8];
+  if (P1.lng) {
+    rv_load(g1, P1.lng, P1.K, lane);
+    rv_load(bb1, P1.lnb, P1.K, lane);
+  }
+  if (P2.lng) {
+    rv_load(g2, P2.lng, P2.K, lane);
+    rv_load(bb2, P2.lnb, P2.K, lane);
+  }
+  real_mask(rm1, P1.K, lane);
+  real_mask(rm2, P2.K, lane);
+  const float bia1 = gld(P1.b + min(o0 + (lane & 3), P1.N - 1));
+  const float bia2 = gld(P2.b + min(o0 + (lane & 3), P2.N - 1));
+  // the head's weights (any workgroup may arrive last): rows 0..7 of W4, LN2 affine, biases; a
+  // head of more outputs loads the rest in its loop (in the loop, each row was a dependent round trip)
+  const HeadProb& H = a.head[k];
+  constexpr int kPre = 8;
+  float w4[kPre][8], hg[8], hb[8];
+#pragma unroll
+  for (int o = 0; o < kPre; ++o) rv_load(w4[o], H.W4 + (size_t)min(o, H.nout - 1) * H.ldw, H.ldw, lane);
+  if (H.lng) {
+    rv_load(hg, H.lng, H.ldh, lane);
+    rv_load(hb, H.lnb, H.ldh, lane);
+  }
+  const float b4 = lane < H.nout ? gld(H.b4 + lane) : 0.f;
+  // 1. H0 of every query row: 4-column partial dot products, summed over the TPR threads of a row
+  //    (butterfly), + b0, ReLU; rows past N0 are zero
+#pragma unroll
+  for (int i = 0; i < NPASS; ++i) {
+    const int o = rsub + RPP * i;
+    const float4 w = w0r[i];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float z = w.x * xr[r][0];
+      z = z + w.y * xr[r][1];
+      z = z + w.z * xr[r][2];
+      z = z + w.w * xr[r][3];
+#pragma unroll
+      for (int m = TPR / 2; m >= 1; m >>= 1) z = z + __shfl_xor(z, m);
+      if (kg == 0) h0[r][o] = o < a.g.N0 ? fmaxf(z + b0r[i], 0.f) : 0.f;
+    }
+  }
+  __syncthreads();
+  TL_MARK(5);
+  const int j = lane & 3, rr = lane >> 2;                // lane 4r + j: column o0 + j of row r
+  // 2. layer 1
+  if (o0 < P1.N) {
+    float x[R][8];
+#pragma unroll
+    for (int r = 0; r < R; ++r) rv_load_lds(x[r], h0[r], P1.K, lane);
+    if (P1.lng) {
+      float mean[R], rstd[R];
+      ln_fwd_rows_pk<R>(x, g1, bb1, rm1, 1.0f / (float)P1.K, mean, rstd);
+    }
+    float z[4][R];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int r = 0; r < R; ++r) z[jj][r] = wsum(rv_pdot(x[r], w1[jj], P1.K, lane));
+    if (rr < R && rr < B && o0 + j < P1.N) {
+      float v = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (jj == j && r == rr) v = z[jj][r];
+      ast(P1.Y + (size_t)rr * P1.ldy + o0 + j, fmaxf(v + bia1, 0.f));
+    }
+  }
+  // 3. hand-off of H1 (every wave's stores drained before the barrier; one add per workgroup)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  TL_MARK(6);
+  const int nb = (int)gridDim.x;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add((GAS int*)c1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    for (int spin = 0; __hip_atomic_load((GAS int*)c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nb; ++spin) {
+      if (spin > (1 << 22)) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    s_flag = ok;
+  }
+  __syncthreads();
+  TL_MARK(7);
+  const bool ok1 = s_flag != 0;
+  // 4. layer 2 on the H1 rows
+  if (o0 < P2.N) {
+    float x[R][8];
+#pragma unroll
+    for (int r = 0; r < R; ++r) rv_load_sc1(x[r], P2.X + (size_t)min(r, B - 1) * P2.ldx, P2.K, lane);
+    if (P2.lng) {
+      float mean[R], rstd[R];
+      ln_fwd_rows_pk<R>(x, g2, bb2, rm2, 1.0f / (float)P2.K, mean, rstd);
+    }
+    float z[4][R];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int r = 0; r < R; ++r) z[jj][r] = wsum(rv_pdot(x[r], w2[jj], P2.K, lane));
+    if (rr < R && rr < B && o0 + j < P2.N) {
+      float v = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (jj == j && r == rr) v = z[jj][r];
+      ast(P2.Y + (size_t)rr * P2.ldy + o0 + j, ok1 ? fmaxf(v + bia2, 0.f) : __builtin_nanf(""));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  TL_MARK(1);
+  if (threadIdx.x == 0)
+    s_flag = __hip_atomic_fetch_add((GAS int*)c2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+  __syncthreads();
+  TL_MARK(2);
+  if (!s_flag) return;
+  // 5. the last arriver: LN2 + head of row `wave` (head_kernel's arithmetic on sc1 loads)
+  if (wave < B) {
+    float x[1][8], mean[1], rstd[1];
+    rv_load_sc1(x[0], H.H3 + (size_t)wave * H.ldh, H.K3, lane);
+    if (H.lng) ln_fwd_rows<1>(x, hg, hb, H.K3, lane, mean, rstd);
+    float zl = 0.f;
+#pragma unroll
+    for (int o = 0; o < kPre; ++o) {
+      if (o >= H.nout) break;
+      const float z = wsum(rv_pdot(x[0], w4[o], H.K3, lane)) + __shfl(b4, o);
+      if (lane == o) zl = z;
+    }
+    for (int o = kPre; o < H.nout; ++o) {
+      float w[8];
+      rv_load(w, H.W4 + (size_t)o * H.ldw, H.ldw, lane);
+      const float z = wsum(rv_pdot(x[0], w, H.K3, lane)) + __shfl(b4, o);
+      if (lane == o) zl = z;
+    }
+    if (lane < H.nout) {
+      if (H.mode == kHeadPolicy) gst(H.out + ((size_t)wave * H.ldo + H.out_col + lane), a.max_action * tanhf(zl));
+      else gst(H.out + ((size_t)wave * H.ldo + lane), zl);
+    }
+  }
+  // publish: the outputs (mapped host memory) complete, a system-scope release, then this network's
+  // flag = the launch's sequence number, which the host polls instead of a stream synchronize
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store((GAS int*)c1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next
+    __hip_atomic_store((GAS int*)c2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // launch (stream order)
+    if (a.flag) {
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.flag + k, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  TL_MARK(3);
 }
 
 // templated on NORM and with the problems in the kernel arguments: a runtime `norm` select on
@@ -2978,6 +3510,42 @@ int launch_gemm2(int m1, int w1, int p1, const GemmTable& t1, int nb1, int m2, i
   return 0;
 }
 
+// the 16-row fused layer-0 stages: NCT x WK = (5, 2) (80 columns, 10 waves) or (2, 4) (32 columns, 8)
+int l0r16_lds_bytes(int Kp, int nct, int wk) {
+  return 4 * (2 * 16 * lds_stride(Kp) + 16 * kR16XS + nct * wk * 16 * 17);
+}
+int launch_l0r16(int nct, int wk, int gather, const GemmTable& t, int nblocks, int Bp, Counters* bump, int bump_actor,
+                 hipStream_t s) {
+  if (nblocks <= 0) return 0;
+  if (Bp % 16 != 0) {
+    set_error("launch_l0r16: Bp %d is not a multiple of 16", Bp);
+    return -1;
+  }
+  for (int k = 0; k < t.nprob; ++k)
+    if (t.p[k].Kp > 512 || t.p[k].exi[6] < 1 || t.p[k].exi[6] > 32 || t.p[k].exi[5] > 512 || t.p[k].exi[5] != t.p[k].Kp) {
+      set_error("launch_l0r16: unsupported layer-0/1 shape (K0 %d, N0p %d, Kp %d)", t.p[k].exi[6], t.p[k].exi[5],
+                t.p[k].Kp);
+      return -1;
+    }
+  const int padded = (nblocks + 7) & ~7;
+  const int tb1 = t.nprob > 1 ? t.p[1].tile_begin : nblocks, tb2 = t.nprob > 2 ? t.p[2].tile_begin : nblocks;
+  const int tb3 = t.nprob > 3 ? t.p[3].tile_begin : nblocks;
+  const int lds = l0r16_lds_bytes(512, nct, wk);
+  const dim3 grid(padded), block(64 * nct * wk);
+  if (nct == 5 && wk == 2) {
+    if (gather) hipLaunchKernelGGL((l0r16_kernel<5, 2, true>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
+    else hipLaunchKernelGGL((l0r16_kernel<5, 2, false>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
+  } else if (nct == 2 && wk == 4) {
+    if (gather) hipLaunchKernelGGL((l0r16_kernel<2, 4, true>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
+    else hipLaunchKernelGGL((l0r16_kernel<2, 4, false>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
+  } else {
+    set_error("launch_l0r16: no (%d, %d) instantiation", nct, wk);
+    return -1;
+  }
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds,
                 Counters* bump, int bump_actor, hipStream_t s) {
   if (nblocks <= 0) return 0;
@@ -3073,6 +3641,45 @@ int launch_gemv(const GemvArgs& a, int nprob, hipStream_t s) {
   if (a.B == 1) hipLaunchKernelGGL(gemv_kernel<1>, grid, dim3(256), 0, s, a);
   else if (a.B == 2) hipLaunchKernelGGL(gemv_kernel<2>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(gemv_kernel<4>, grid, dim3(256), 0, s, a);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_act(const ActArgs& a, int nprob, hipStream_t s) {
+  const int B = a.g.l1.B;
+  int N1 = 0;
+  bool ok = nprob >= 1 && nprob <= 2 && B >= 1 && B <= kGemvRows && a.g.K0 >= 1 && a.g.K0 <= kGemv0K &&
+            a.g.N0 >= 1 && a.g.N0 <= 512 && a.ctr;
+  for (int k = 0; ok && k < nprob; ++k) {
+    const GemvProb &p1 = a.g.l1.p[k], &p2 = a.l2[k];
+    const HeadProb& hd = a.head[k];
+    N1 = std::max(N1, p1.N);
+    ok = p1.K == a.g.N0 && p1.N >= 1 && p1.N <= 512 && p2.K == p1.N && p2.X == p1.Y && p2.N >= 1 && p2.N <= p1.N &&
+         hd.H3 == p2.Y && hd.K3 == p2.N && hd.nout >= 1 && hd.nout <= 64 && hd.ldw <= 512;
+  }
+  if (!ok) {
+    set_error("launch_act: unsupported query shape (%d problems, %d rows, layer 0 %d -> %d)", nprob, B, a.g.K0, a.g.N0);
+    return -1;
+  }
+  for (int k = 1; k < nprob; ++k)
+    if (a.g.l1.p[k].N != N1) {
+      set_error("launch_act: networks of one launch need the same layer-1 width");
+      return -1;
+    }
+  const dim3 grid((N1 + 15) / 16, nprob);
+  if (a.g.ldw0 < (a.g.K0 <= 32 ? 32 : 64)) {
+    set_error("launch_act: layer-0 rows of %d floats (K0 %d)", a.g.ldw0, a.g.K0);
+    return -1;
+  }
+  if (a.g.K0 <= 32) {
+    if (B == 1) hipLaunchKernelGGL((act_kernel<1, 8>), grid, dim3(256), 0, s, a);
+    else if (B == 2) hipLaunchKernelGGL((act_kernel<2, 8>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((act_kernel<4, 8>), grid, dim3(256), 0, s, a);
+  } else {
+    if (B == 1) hipLaunchKernelGGL((act_kernel<1, 16>), grid, dim3(256), 0, s, a);
+    else if (B == 2) hipLaunchKernelGGL((act_kernel<2, 16>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((act_kernel<4, 16>), grid, dim3(256), 0, s, a);
+  }
   TD3_HIP(hipGetLastError());
   return 0;
 }
@@ -3227,7 +3834,9 @@ int kernels_init() {
   if (rc) return rc;
   for (const void* f : {(const void*)gemm_kernel<0, kWn4x2, kProCopy>, (const void*)gemm_kernel<0, kWn4x2, kProLN>,
                         (const void*)gemm_kernel<1, kWn4x2, kProCopy>, (const void*)gemm_kernel<1, kWn4x2, kProLNBwd>,
-                        (const void*)gemm_kernel<1, kWn4x2, kProHeadBwd>})
+                        (const void*)gemm_kernel<1, kWn4x2, kProHeadBwd>,
+                        (const void*)l0r16_kernel<5, 2, true>, (const void*)l0r16_kernel<5, 2, false>,
+                        (const void*)l0r16_kernel<2, 4, true>, (const void*)l0r16_kernel<2, 4, false>})
     TD3_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   return 0;
 }
@@ -3241,6 +3850,20 @@ extern "C" int td3_tl_read(unsigned long long* out, int n) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(td3::td3_tl), (size_t)n * 8 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
+  return 0;
+}
+extern "C" int td3_clk_read(unsigned long long* out, int n) {
+  if (n > 8192) n = 8192;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(td3::td3_clk), (size_t)n * 2 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return 0;
+}
+extern "C" int td3_clk_sum_read(unsigned long long* out, int clear) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(td3::td3_clk_sum), 16, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  static const unsigned long long z[2] = {0, 0};
+  if (clear && hipMemcpyToSymbol(HIP_SYMBOL(td3::td3_clk_sum), z, 16, 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
   return 0;
 }
 extern "C" int td3_tl_clear() {

@@ -20,6 +20,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <functional>
@@ -63,6 +65,8 @@ struct TensorRef { std::string name; int64_t rows, cols; int64_t off; int ld; };
 
 struct Group {
   int64_t size = 0;          // floats per arena copy
+  int64_t cap = 0;           // allocated floats per copy (>= size + 256: the sharded optimizer's
+                             // rank slices of 4-float multiples may run past `size` into zero pads)
   float *P = nullptr, *T = nullptr, *M = nullptr, *V = nullptr, *G = nullptr;
   std::vector<NetL> nets;
   std::vector<TensorRef> tensors;
@@ -193,6 +197,9 @@ struct Stage {
   // on its own stream after the fixed-order sum (RCCL mode: both queued on the comm stream)
   int64_t coll_off = 0, coll_n = -1;
   std::function<int(hipStream_t)> after;
+  // the sharded optimizer step (reduce-scatter -> Adam on the rank's slice -> all-gather of the
+  // parameters): the slice length; the seam copies each owner's parameter slice to the others
+  int64_t coll_slice = 0;
 };
 
 // Replicas of one process sharing a device (td3_comm_init_local): the test seam of the data-parallel
@@ -281,6 +288,12 @@ struct ActPlan {       // select_action / eval_q at small batch
   GemvArgs gv_act[3], gv_q[3];
   Gemv01Args g01_act{}, g01_q{};
   HeadArgs head_act{}, head_q{};
+  // the same query as ONE launch (act_kernel): select_action / eval_q (separate counters: they run
+  // on different streams)
+  bool act1 = false;
+  ActArgs a1_act{}, a1_q{};
+  unsigned* hflag[2] = {nullptr, nullptr};    // host views of a1_act.flag / a1_q.flag (mapped)
+  unsigned seq[2] = {0, 0};
   int64_t* d_iota = nullptr;
   EvalB A, Q[2];
   std::vector<void*> tables;
@@ -343,6 +356,8 @@ struct td3_handle {
                                               // query ran (act_used): an event record costs the
                                               // step's stream ~4 us, pure training needs none
   bool act_used = false;
+  uint64_t actor_ev_seq = 0;                  // actor_ev records so far / the one the acting stream
+  uint64_t act_wait_seq = ~0ull;              // last waited for (no second wait on the same record)
   hipStream_t last_step_stream = nullptr;     // the stream of the last train step
   std::unique_ptr<Plan> plan;
   std::map<int, std::unique_ptr<ActPlan>> act;
@@ -351,9 +366,11 @@ struct td3_handle {
   // optimizer steps run on comm_stream, ordered after the bucket's dW by comm_ev (recorded on the step
   // stream) and joined back by comm_done before the next stage that reads the parameters
   hipStream_t comm_stream = nullptr;
-  hipEvent_t comm_ev = nullptr, comm_done = nullptr;
+  hipEvent_t comm_ev = nullptr, comm_ev1 = nullptr, comm_done = nullptr;
   std::shared_ptr<LocalGroup> local;          // td3_comm_init_local (comm stays null)
   int nranks = 1, rank = 0;
+  bool dp_sharded = false;                    // the plan's optimizer steps are sharded (add_dw_stage)
+  int64_t opt_gathered_it = -1;               // total_it of the last td3_dp_gather_optimizer_state
   std::vector<Stage>* last_body = nullptr;
   Ring* last_ring = nullptr;                  // the ring of the last td3_profile_stages (stage 0: its gather)
   uint64_t last_ring_gen = 0;                 // its Ring::gen (td3_time_stage refuses a destroyed ring)
@@ -598,10 +615,37 @@ static bool can_fuse_l0(const std::vector<FwdItem>& items) {
   return true;
 }
 
+// The fused layer-0 stage on 16-row tiles (l0r16_kernel) where it fills the chip in one round:
+// 80-column workgroups (10 waves) when 16-row x 80-column tiles of every network fit 256 workgroups
+// and 32-column ones (8 waves) would not, else 32-column workgroups when those fit (one network:
+// AF_fwd01), else none (the 32-row gemm_body stage).  B < 512 only; TD3_L0R16=0 turns it off.
+static bool l0r16_config(const std::vector<FwdItem>& items, int Bp, int* nct, int* wk) {
+  static const bool on = env_int("TD3_L0R16", 1) != 0;
+  if (!on || Bp >= 512 || Bp % 16) return false;
+  int b80 = 0, b32 = 0;
+  for (auto& it : items) {
+    const LinearL& L = it.net->lin[1];
+    if (L.Kp > 512 || it.net->lin[0].Np != L.Kp) return false;
+    b80 += (Bp / 16) * ((L.N + 79) / 80);
+    b32 += (Bp / 16) * ((L.N + 31) / 32);
+  }
+  if (b32 <= 256) {
+    *nct = 2;
+    *wk = 4;
+    return true;
+  }
+  if (b80 <= 256) {
+    *nct = 5;
+    *wk = 2;
+    return true;
+  }
+  return false;
+}
+
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
                           Counters* bump, int bump_actor, const RingSide* ring = nullptr,
-                          const RingOut* ro = nullptr, int o_r = 0, bool fuse_l0 = false) {
+                          const RingOut* ro = nullptr, int o_r = 0, bool fuse_l0 = false, bool r16 = false) {
   const bool norm = h->cfg.norm == 1;
   fuse_l0 = fuse_l0 && can_fuse_l0(items);
   for (int l = fuse_l0 ? 1 : 0; l < 3; ++l) {
@@ -718,6 +762,44 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     }
     // the step counters are bumped by the launch after the one that draws the sample
     const int bump_l = fuse_l0 ? 2 : 1;
+    int nct = 0, wk = 0;
+    if (l0 && r16 && l0r16_config(items, Bp, &nct, &wk)) {
+      // the same problems on 16-row tiles of 16*nct real layer-1 columns (the pad columns of H1 are
+      // zero from the scratch's creation and no stage writes them)
+      int nb16 = 0;
+      for (auto& p : probs) {
+        const int nreal = items[&p - probs.data()].net->lin[1].N;
+        p.ntiles = (nreal + 16 * nct - 1) / (16 * nct);
+        p.tile_begin = nb16;
+        p.Nout = std::min(p.Nout, p.ntiles * 16 * nct);
+        nb16 += (Bp / 16) * p.ntiles;
+      }
+      GemmTable t{};
+      for (size_t i = 0; i < probs.size(); ++i) t.p[i] = probs[i];
+      t.nprob = (int)probs.size();
+      char kname[64];
+      snprintf(kname, sizeof(kname), "td3::l0r16_kernel<%d, %d, %s>", nct, wk, gather ? "true" : "false");
+      Counters* bmp = l == bump_l ? bump : nullptr;
+      const std::string name = std::string(tag) + "_fwd01";
+      if (gather) {
+        const RingSide* rs = ring;
+        st.push_back({name,
+                      [=](hipStream_t s) {
+                        GemmTable tt = t;
+                        tt.rs = *rs;
+                        if (!tt.rs.data) {
+                          set_error("internal: ring-sampled stage launched without a bound ring");
+                          return -1;
+                        }
+                        return launch_l0r16(nct, wk, 1, tt, nb16, Bp, bmp, bump_actor, s);
+                      },
+                      flops, kname});
+      } else {
+        st.push_back({name, [=](hipStream_t s) { return launch_l0r16(nct, wk, 0, t, nb16, Bp, bmp, bump_actor, s); },
+                      flops, kname});
+      }
+      continue;
+    }
     TD3_RC(push_gemm_stage(h, owned, st, probs, 0, wn, pro, Bp, lds, blocks, flops,
                            std::string(tag) + (l0 ? "_fwd01" : "_fwd" + std::to_string(l)),
                            l == bump_l ? bump : nullptr, bump_actor, gather ? ring : nullptr));
@@ -868,6 +950,15 @@ static bool dp_overlap(const td3_handle* h) {
   if (h->local) return true;
   return h->comm && (h->nranks > 1 || m >= 2);
 }
+
+// The data-parallel optimizer step: sharded (reduce-scatter -> Adam on the rank's 1/N slice ->
+// all-gather of the parameters; TD3_DP_SHARD=1, the default) or all-reduce -> replicated flat Adam
+// (0).  Weight normalization and the bucketed schedule keep the all-reduce.  Read at plan build.
+static bool dp_shard(const td3_handle* h) {
+  (void)h;
+  return env_int("TD3_DP_SHARD", 1) != 0;
+}
+static int64_t shard_slice(const Group& g, int nranks) { return ((g.size + 4 * nranks - 1) / (4 * nranks)) * 4; }
 
 // The split-K partition of a dW stage's problems (kernels.h DwSplit): every tile's 64-row steps in
 // one weighted list, cut evenly over one workgroup per CU; per problem its tm x tm matrix tiles (n tile
@@ -1037,17 +1128,17 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   if (dp && split && !wn && enc_nwg == 0 && items.size() == 2 && dp_overlap(h)) {
     // The overlapped data-parallel schedule for a twin critic: one bucket per network
     // in arena order.  Stages: dW_0 (split-K, gradient only; then an event on the step stream),
-    // dW_1, bucket 0's all-reduce + Adam (+ Polyak) on the comm stream behind that event, bucket 1's
-    // on the step stream, then the join (the step stream waits for the comm stream's Adam).
+    // dW_1 (then a second event), bucket 0's all-reduce + Adam (+ Polyak) on the comm stream behind
+    // the first event, bucket 1's on the comm stream behind the second (one RCCL stream per
+    // communicator: ADVICE r04), then the join (the step stream waits for bucket 1's Adam).
     // Bucket 0's exchange runs under dW_1; dW_1 is enqueued before the host makes bucket 0's RCCL
-    // call, and the last bucket stays on the step stream, so neither costs a stream hop on the
-    // critical path.  The in-process seam runs the same buckets: a fixed-order sum of the range,
-    // then the bucket's optimizer step (Stage::after), on its one stream.
+    // call.  The in-process seam runs the same buckets: a fixed-order sum of the range, then the
+    // bucket's optimizer step (Stage::after), on its one stream.
     const bool local = h->local != nullptr;
     ncclComm_t comm = h->comm;
     hipStream_t cs = h->comm_stream;
-    hipEvent_t ev = h->comm_ev, done = h->comm_done;
-    TD3_ARG(local || (cs && ev && done), "internal: data-parallel handle without a comm stream");
+    hipEvent_t ev = h->comm_ev, ev1 = h->comm_ev1, done = h->comm_done;
+    TD3_ARG(local || (cs && ev && ev1 && done), "internal: data-parallel handle without a comm stream");
     const int pol = polyak ? 1 : 0;
     const std::string kname = std::string("td3::dwsk_kernel<") + (unit_scale ? "true, " : "false, ") +
                               (tm == 128 ? "true>" : "false>");
@@ -1073,7 +1164,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                       DwSplit kk = kb;
                       kk.slab = slab->p;
                       TD3_RC(launch_dw_split(ab, kk, s));
-                      if (first && !local) TD3_HIP(hipEventRecord(ev, s));
+                      if (!local) TD3_HIP(hipEventRecord(first ? ev : ev1, s));
                       return 0;
                     },
                     fb, kname});
@@ -1093,15 +1184,16 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                   set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
                   return -1;
                 }
-                hipStream_t q = first ? cs : s;
-                if (first) TD3_HIP(hipStreamWaitEvent(cs, ev, 0));
-                ncclResult_t r = ncclAllReduce(Gb, Gb, (size_t)nb, ncclFloat, ncclSum, comm, q);
+                // both buckets on the comm stream (one RCCL stream per communicator),
+                // each behind its own dW; the join waits for the last bucket's Adam
+                TD3_HIP(hipStreamWaitEvent(cs, first ? ev : ev1, 0));
+                ncclResult_t r = ncclAllReduce(Gb, Gb, (size_t)nb, ncclFloat, ncclSum, comm, cs);
                 if (r != ncclSuccess) {
                   set_error("ncclAllReduce: %s", ncclGetErrorString(r));
                   return -2;
                 }
-                TD3_RC(launch_adam_flat(ar, nb, pol, q));
-                if (first) TD3_HIP(hipEventRecord(done, cs));
+                TD3_RC(launch_adam_flat(ar, nb, pol, cs));
+                if (!first) TD3_HIP(hipEventRecord(done, cs));
                 return 0;
               },
               0, "rccl"};
@@ -1153,6 +1245,59 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     st.push_back({std::string(tag) + "_enc_adam", [=](hipStream_t s) { return launch_enc_adam(ea, s); }, 0,
                   "td3::enc_adam_kernel"});
   }
+  AdamArgs aa = a.adam;
+  if (dp) aa.grad_scale = 1.0f / (float)h->nranks;
+  const int pol = polyak ? 1 : 0;
+  if (dp && !wn && dp_shard(h)) {
+    // Sharded optimizer step (ZeRO-1 form): the summed gradient reaches only this
+    // rank's slice (ncclReduceScatter, in place), Adam runs on that slice alone (the moments of the
+    // other slices live on their owners), ncclAllGather brings every rank the updated parameters,
+    // then Polyak runs replicated over the whole arena (the same inputs on every rank: the replicas
+    // stay bit-identical, each element computed once).  Same bytes on the links as the all-reduce,
+    // one extra collective launch, 1/N of the Adam pass.
+    const int N = h->nranks, R = h->rank;
+    const int64_t slice = shard_slice(g, N);
+    TD3_ARG(N * slice <= g.cap, "internal: shard slices past the arena");
+    h->dp_sharded = true;
+    ncclComm_t comm = h->comm;
+    float* G = g.G;
+    float* Pp = g.P;
+    const bool local = h->local != nullptr;
+    AdamArgs as = aa;
+    as.P += R * slice; as.G += R * slice; as.M += R * slice; as.V += R * slice; as.T += R * slice;
+    Stage x{std::string(tag) + "_rs_adam_ag",
+            [=](hipStream_t s) {
+              if (local) {
+                set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
+                return -1;
+              }
+              ncclResult_t r = ncclReduceScatter(G, G + R * slice, (size_t)slice, ncclFloat, ncclSum, comm, s);
+              if (r != ncclSuccess) {
+                set_error("ncclReduceScatter: %s", ncclGetErrorString(r));
+                return -2;
+              }
+              TD3_RC(launch_adam_flat(as, slice, 0, s));
+              r = ncclAllGather(Pp + R * slice, Pp, (size_t)slice, ncclFloat, comm, s);
+              if (r != ncclSuccess) {
+                set_error("ncclAllGather: %s", ncclGetErrorString(r));
+                return -2;
+              }
+              return 0;
+            },
+            0, "rccl"};
+    x.collective = which == 1 ? 0 : 1;
+    x.coll_slice = slice;
+    x.after = [=](hipStream_t s) { return launch_adam_flat(as, slice, 0, s); };
+    st.push_back(x);
+    if (polyak) {
+      float* Tp = g.T;
+      const int64_t n = g.size;
+      const float tau = (float)h->cfg.tau;
+      st.push_back({std::string(tag) + "_polyak", [=](hipStream_t s) { return launch_polyak_flat(Tp, Pp, n, tau, s); },
+                    0, "td3::polyak_flat_kernel"});
+    }
+    return 0;
+  }
   if (dp) {
     ncclComm_t comm = h->comm;
     float* G = g.G;
@@ -1174,9 +1319,6 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                   0, "rccl"});
     st.back().collective = which == 1 ? 0 : 1;     // AdamArgs::which 1 = actor -> group 0
   }
-  AdamArgs aa = a.adam;
-  if (dp) aa.grad_scale = 1.0f / (float)h->nranks;
-  const int pol = polyak ? 1 : 0;
   if (wn) {
     WnArgs w = g.wn;
     w.adam = aa;
@@ -1338,7 +1480,8 @@ static int build_step(td3_handle* h, int B) {
       std::vector<FwdItem> f1 = {{&an, Pta, &P->TA, false, false}, {&q1, Pq1, &P->Q[0], true, true},
                                  {&q2, Pq2, &P->Q[1], true, true}};
       if (actor_phase) f1.push_back({&an, Pa, &P->A, true, true});
-      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase, nullptr, nullptr, 0, true));
+      TD3_RC(add_fwd_stages(h, P->tables, st, f1, Bp, B, "F", h->d_ctr, actor_phase, nullptr, nullptr, 0, true,
+                            true));
       {  // the ring-sampled first layer (record layout [s | a | s' | r | not_done], replay.hip)
         // the first column tile of each problem keeps what the later stages read: the target-twin
         // input s' (X_S2A), the twin (and actor) dW input [s | a] (X_SA), reward / not_done, and on
@@ -1354,7 +1497,7 @@ static int build_step(td3_handle* h, int B) {
                          {nullptr, 0, nullptr, 0, P->R, P->ND},
                          {P->X_SP, P->ld_sa, nullptr, 0, nullptr, nullptr}};
         TD3_RC(add_fwd_stages(h, P->tables, fr, f1r, Bp, B, "F", h->d_ctr, actor_phase, &P->rside, ro,
-                              2 * sd + ad, true));
+                              2 * sd + ad, true, true));
         P->body_ring[actor_phase][inj].push_back(fr[0]);
       }
       if (kUnitCritic) {
@@ -1503,7 +1646,7 @@ static int build_step(td3_handle* h, int B) {
         f3[0].tcol = sd;
         f3[0].tn = ad;
       }
-      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0, nullptr, nullptr, 0, true));
+      TD3_RC(add_fwd_stages(h, P->tables, st, f3, Bp, B, "AF", nullptr, 0, nullptr, nullptr, 0, true, true));
       // the actor loss -mean Q1(s, pi(s)) (:159): Q1's head and its backward are the prologue of
       // AQB_bwd2 (kProHeadBwd; the row launch kRowActorLoss is the particle path's)
       std::vector<BwdItem> aqb = {{&q1, Pq1, &P->AQ, false}};
@@ -2127,6 +2270,7 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
 static int build_step_particles(td3_handle* h, int B);
 
 static int build_plan(td3_handle* h, int B) {
+  h->dp_sharded = false;                      // set again by add_dw_stage when it shards
   // the profiled stage list lives in the plan being replaced
   h->last_body = nullptr;
   h->last_ring = nullptr;
@@ -2168,7 +2312,10 @@ static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_s
   h->last_step_stream = s;
   if (actor_phase) {
     h->actor_step += 1;
-    if (h->act_used) TD3_HIP(hipEventRecord(h->actor_ev, s));
+    if (h->act_used) {
+      TD3_HIP(hipEventRecord(h->actor_ev, s));
+      ++h->actor_ev_seq;
+    }
   }
   if (!stats) return 0;
   Plan* P = h->plan.get();
@@ -2206,6 +2353,8 @@ static int finish_step(td3_handle* h, int actor_phase, hipStream_t s, td3_step_s
 }
 
 // ------------------------------------------------------------------ act / eval_q plans
+// select_action / eval_q of <= kGemvRows rows as one act_kernel launch (TD3_ACT1=1, the default) or
+// the gemv01 -> gemv -> head chain of three launches (0: the A/B reference; read when a plan is built)
 static int build_act(td3_handle* h, int Bp, ActPlan** out) {
   auto it = h->act.find(Bp);
   if (it != h->act.end()) {
@@ -2219,7 +2368,7 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
   const NetL& q1 = h->critic.nets[0];
   const NetL& q2 = h->critic.nets[1];
   const int lds_s = pad32(h->sd), lds_sa = pad32(h->sd + h->ad);
-  const size_t io_floats = (size_t)Bp * (lds_s + lds_sa + h->ad + 2) + 4 * 64;
+  const size_t io_floats = (size_t)Bp * (lds_s + lds_sa + h->ad + 2) + 8 * 64;   // + the one-launch query flags
   size_t floats = io_floats + eval_floats(an, Bp, false, norm) + 2 * eval_floats(q1, Bp, false, norm) + 4096;
   TD3_HIP(hipMalloc(&A->scratch, floats * 4));
   TD3_HIP(hipMemset(A->scratch, 0, floats * 4));
@@ -2325,6 +2474,43 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     a.max_action = h->cfg.max_action;
     A->head_q = a;
     A->evalq.push_back({"evq_head", [=](hipStream_t s) { return launch_heads(a, 2, s); }, 0});
+  }
+  // one-launch queries: layer 2 rides on the layer-1 column groups (N2 <= N1, same N1 for the twins)
+  if (A->gemv01 && env_int("TD3_ACT1", 1) != 0) {
+    int* ctr = reinterpret_cast<int*>(S.take(64));      // zeroed with the scratch
+    auto mk = [&](ActArgs& a, const Gemv01Args& g, const GemvArgs& l2, std::initializer_list<const NetL*> nets,
+                  const float* Pp, EvalB* const* ev, float* const* outs, int ldo, int mode, int* c) {
+      a = ActArgs{};
+      a.g = g;
+      a.ctr = c;
+      a.max_action = h->cfg.max_action;
+      int k = 0;
+      bool ok = true;
+      for (const NetL* n : nets) {
+        a.l2[k] = l2.p[k];
+        HeadProb q = head(*n, Pp, *ev[k], mode);
+        q.out = outs[k];
+        q.ldo = ldo;
+        q.out_col = 0;
+        a.head[k] = q;
+        ok = ok && n->lin[2].N <= n->lin[1].N && n->lin[1].N == nets.begin()[0]->lin[1].N && n->lin[3].N <= 64;
+        ++k;
+      }
+      return ok;
+    };
+    EvalB* ea[1] = {&A->A};
+    float* oa[1] = {A->out};
+    EvalB* eq[2] = {&A->Q[0], &A->Q[1]};
+    float* oq[2] = {A->q[0], A->q[1]};
+    A->act1 = A->hio && mk(A->a1_act, A->g01_act, A->gv_act[2], {&an}, h->actor.P, ea, oa, A->ldo, kHeadPolicy, ctr) &&
+              mk(A->a1_q, A->g01_q, A->gv_q[2], {&q1, &q2}, h->critic.P, eq, oq, 1, kHeadQ, ctr + 8);
+    if (A->act1) {       // completion flags in the mapped block (io_floats reserves 4 * 64 floats of slack)
+      float* hf = nullptr;
+      A->a1_act.flag = reinterpret_cast<unsigned*>(io.take(64, &hf));
+      A->hflag[0] = reinterpret_cast<unsigned*>(hf);
+      A->a1_q.flag = reinterpret_cast<unsigned*>(io.take(64, &hf));
+      A->hflag[1] = reinterpret_cast<unsigned*>(hf);
+    }
   }
   *out = A.get();
   h->act[Bp] = std::move(A);
@@ -2567,7 +2753,9 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
     h->critic.nets.push_back(layout_mlp(h->sd + h->ad, cfg->critic_hidden, 1, norm, "q2.", off, h->critic.tensors));
     h->critic.size = off;
   }
-  const size_t total = 5 * (size_t)(h->actor.size + h->critic.size);
+  h->actor.cap = ((h->actor.size + 255) & ~(int64_t)255) + 256;
+  h->critic.cap = ((h->critic.size + 255) & ~(int64_t)255) + 256;
+  const size_t total = 5 * (size_t)(h->actor.cap + h->critic.cap);
   hipError_t e = hipMalloc(&h->arena, total * sizeof(float));
   if (e != hipSuccess) {
     set_error("td3_create: hipMalloc failed: %s", hipGetErrorString(e));
@@ -2577,11 +2765,11 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   TD3_HIP(hipMemset(h->arena, 0, total * sizeof(float)));
   float* p = h->arena;
   for (Group* g : {&h->actor, &h->critic}) {
-    g->P = p; p += g->size;
-    g->T = p; p += g->size;
-    g->M = p; p += g->size;
-    g->V = p; p += g->size;
-    g->G = p; p += g->size;
+    g->P = p; p += g->cap;
+    g->T = p; p += g->cap;
+    g->M = p; p += g->cap;
+    g->V = p; p += g->cap;
+    g->G = p; p += g->cap;
   }
   TD3_HIP(hipMalloc(&h->d_ctr, sizeof(Counters)));
   {
@@ -2629,6 +2817,7 @@ int td3_destroy(td3_handle* h) {
     (void)hipStreamSynchronize(h->comm_stream);
     (void)hipStreamDestroy(h->comm_stream);
     (void)hipEventDestroy(h->comm_ev);
+    (void)hipEventDestroy(h->comm_ev1);
     (void)hipEventDestroy(h->comm_done);
   }
   if (h->comm) ncclCommDestroy(h->comm);
@@ -2688,6 +2877,53 @@ static int which_ptr(td3_handle* h, int which, Group** g, float** base) {
   return -1;
 }
 
+// Sharded optimizer state (the Adam moments of slice k live on rank k): the in-process seam copies
+// the other replicas' slices in before a moment is read; RCCL ranks gather them with the collective
+// td3_dp_gather_optimizer_state, which a read of the moments then requires.
+static int consolidate_moments(td3_handle* h, int which) {
+  if (!h->dp_sharded || h->nranks <= 1) return 0;
+  const bool m = which == TD3_ACTOR_ADAM_M || which == TD3_CRITIC_ADAM_M;
+  const bool v = which == TD3_ACTOR_ADAM_V || which == TD3_CRITIC_ADAM_V;
+  if (!m && !v) return 0;
+  const bool actor = which == TD3_ACTOR_ADAM_M || which == TD3_ACTOR_ADAM_V;
+  if (h->local) {
+    const int64_t sl = shard_slice(actor ? h->actor : h->critic, h->nranks);
+    for (int k = 0; k < (int)h->local->hs.size(); ++k) {
+      td3_handle* o = h->local->hs[k];
+      if (o == h || !o) continue;
+      const Group& src = actor ? o->actor : o->critic;
+      const Group& dst = actor ? h->actor : h->critic;
+      TD3_HIP(hipMemcpy((m ? dst.M : dst.V) + k * sl, (m ? src.M : src.V) + k * sl, (size_t)sl * 4,
+                        hipMemcpyDeviceToDevice));
+    }
+    return 0;
+  }
+  TD3_ARG(h->opt_gathered_it == h->total_it,
+          "sharded optimizer state: call td3_dp_gather_optimizer_state on every rank before reading the "
+          "Adam moments (a collective)");
+  return 0;
+}
+
+int td3_dp_gather_optimizer_state(td3_handle* h) {
+  TD3_ARG(h != nullptr, "null handle");
+  TD3_HIP(hipSetDevice(h->cfg.device));
+  if (h->dp_sharded && h->comm && h->nranks > 1) {
+    for (Group* g : {&h->actor, &h->critic}) {
+      const int64_t sl = shard_slice(*g, h->nranks);
+      for (float* a : {g->M, g->V}) {
+        ncclResult_t r = ncclAllGather(a + h->rank * sl, a, (size_t)sl, ncclFloat, h->comm, h->stream);
+        if (r != ncclSuccess) {
+          set_error("ncclAllGather: %s", ncclGetErrorString(r));
+          return -2;
+        }
+      }
+    }
+    TD3_HIP(hipStreamSynchronize(h->stream));
+  }
+  h->opt_gathered_it = h->total_it;
+  return 0;
+}
+
 int td3_get_params(td3_handle* h, int which, float* out, int64_t n) {
   TD3_ARG(h && out, "null argument");
   Group* g;
@@ -2697,6 +2933,7 @@ int td3_get_params(td3_handle* h, int which, float* out, int64_t n) {
   TD3_HIP(hipSetDevice(h->cfg.device));
   TD3_HIP(hipStreamSynchronize(h->stream));
   TD3_HIP(hipDeviceSynchronize());
+  TD3_RC(consolidate_moments(h, which));
   std::vector<float> host(g->size);
   TD3_HIP(hipMemcpy(host.data(), base, g->size * 4, hipMemcpyDeviceToHost));
   int64_t o = 0;
@@ -2872,6 +3109,29 @@ static int get_rows(float* dst, int cols, const float* dev, const float* host, i
   return 0;
 }
 
+// The one-launch query publishes its outputs with a flag in mapped host memory (act_kernel): the host
+// polls that flag instead of synchronising the stream (a stream sync's wake-up is most of the ~10 us
+// launch + sync round trip, DESIGN "Acting path").  A flag that does not arrive within 2 s falls back
+// to a stream synchronize, then reports an error if it is still missing.
+static int wait_flags(volatile unsigned* f, int nprob, unsigned seq, hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int k = 0; k < nprob; ++k) {
+    int spin = 0;
+    while (f[k] != seq) {
+      __builtin_ia32_pause();
+      if ((++spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        TD3_HIP(hipStreamSynchronize(s));
+        if (f[k] != seq) {
+          set_error("select_action / eval_q: the query kernel's completion flag did not arrive");
+          return -1;
+        }
+      }
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return 0;
+}
+
 // A featured query of n <= kGemvRows rows: layers 0 and 1 in one gemv01 launch when layer 0 is
 // narrow (the query rows [x0 | x1] in its arguments), else one gemv launch per layer; then the
 // head over 4 rows.
@@ -2879,6 +3139,19 @@ static int run_gemv(const ActPlan* A, bool q, int n, const float* x0, int c0, co
                     hipStream_t s) {
   const GemvArgs(&gv)[3] = q ? A->gv_q : A->gv_act;
   const int nprob = q ? 2 : 1;
+  if (A->act1) {                                        // the whole query in one launch
+    ActArgs a = q ? A->a1_q : A->a1_act;
+    a.g.l1.B = n;
+    const int K0 = c0 + c1;
+    for (int r = 0; r < n; ++r) {
+      memcpy(a.g.xq + r * K0, x0 + (size_t)r * c0, (size_t)c0 * 4);
+      if (c1) memcpy(a.g.xq + r * K0 + c0, x1 + (size_t)r * c1, (size_t)c1 * 4);
+    }
+    ActPlan* M = const_cast<ActPlan*>(A);
+    a.seq = ++M->seq[q ? 1 : 0];
+    TD3_RC(launch_act(a, nprob, s));
+    return wait_flags(M->hflag[q ? 1 : 0], nprob, a.seq, s);
+  }
   int l = 0;
   if (A->gemv01) {
     Gemv01Args g = q ? A->g01_q : A->g01_act;
@@ -2908,9 +3181,16 @@ static int run_gemv(const ActPlan* A, bool q, int n, const float* x0, int c0, co
 static int order_after_actor(td3_handle* h, hipStream_t s) {
   if (!h->act_used) {
     h->act_used = true;
-    if (h->last_step_stream) TD3_HIP(hipEventRecord(h->actor_ev, h->last_step_stream));
+    if (h->last_step_stream) {
+      TD3_HIP(hipEventRecord(h->actor_ev, h->last_step_stream));
+      ++h->actor_ev_seq;
+    }
   }
-  TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
+  // a stream wait is a barrier packet (~3.5 us of GPU time on the acting stream even when the event
+  // has completed): none when this record was waited for already, or has completed
+  if (h->act_wait_seq == h->actor_ev_seq) return 0;
+  if (hipEventQuery(h->actor_ev) != hipSuccess) TD3_HIP(hipStreamWaitEvent(s, h->actor_ev, 0));
+  h->act_wait_seq = h->actor_ev_seq;
   return 0;
 }
 
@@ -2922,6 +3202,13 @@ int td3_select_action(td3_handle* h, const float* state, float* action_out, int 
   ActPlan* A;
   TD3_RC(build_act(h, pad32(n), &A));
   hipStream_t s = h->act_stream;
+  if (A->act1 && A->gemv && n <= kGemvRows) {
+    // the query travels in the kernel arguments and the outputs of the previous query were read
+    // before it returned: no stream synchronize on either side (wait_flags)
+    TD3_RC(order_after_actor(h, s));
+    TD3_RC(run_gemv(A, false, n, state, h->sd, nullptr, 0, s));
+    return get_rows(action_out, h->ad, A->out, A->hout, A->ldo, n, s);
+  }
   if (A->hio) TD3_HIP(hipStreamSynchronize(s));
   TD3_RC(order_after_actor(h, s));
   if (A->gemv && n <= kGemvRows) {
@@ -2944,8 +3231,13 @@ int td3_eval_q(td3_handle* h, const float* state, const float* action, float* q_
   TD3_RC(build_act(h, pad32(n), &A));
   hipStream_t s = h->stream;
   const int ld = pad32(h->sd + h->ad);
-  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
   const bool small = A->gemv && n <= kGemvRows;
+  if (A->act1 && small) {        // one launch, completion flags polled on the host (no stream syncs)
+    TD3_RC(run_gemv(A, true, n, state, h->sd, action, h->ad, s));
+    TD3_RC(get_rows(q_out, 1, A->q[0], A->hq[0], 1, n, s));
+    return get_rows(q_out + n, 1, A->q[1], A->hq[1], 1, n, s);
+  }
+  if (A->hio) TD3_HIP(hipStreamSynchronize(s));
   if (!small || !A->gemv01) {
     TD3_RC(put_rows(A, A->X_SA, A->hX_SA, ld, 0, state, n, h->sd, s));
     TD3_RC(put_rows(A, A->X_SA, A->hX_SA, ld, h->sd, action, n, h->ad, s));
@@ -3022,7 +3314,10 @@ int td3_actor_learn_particles(td3_handle* h, const float* feat, const float* par
   TD3_RC(run_stages(P->actor_learn, s));
   h->last_step_stream = s;
   h->actor_step += 1;
-  if (h->act_used) TD3_HIP(hipEventRecord(h->actor_ev, s));
+  if (h->act_used) {
+    TD3_HIP(hipEventRecord(h->actor_ev, s));
+    ++h->actor_ev_seq;
+  }
   if (!actor_loss) return 0;
   TD3_HIP(hipStreamSynchronize(s));
   const int nq = P->nq, ldq = P->ldq;
@@ -3114,6 +3409,7 @@ int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int ra
   if (!h->comm_stream) {
     TD3_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
     TD3_HIP(hipEventCreateWithFlags(&h->comm_ev, hipEventDisableTiming));
+    TD3_HIP(hipEventCreateWithFlags(&h->comm_ev1, hipEventDisableTiming));
     TD3_HIP(hipEventCreateWithFlags(&h->comm_done, hipEventDisableTiming));
   }
   if (h->plan) {           // stage lists change (grad write + all-reduce + flat Adam)
@@ -3223,6 +3519,17 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
     TD3_RC(launch_local_sum(a, s));
     for (int k = 0; k < n; ++k)               // the bucket's optimizer step behind its sum
       if (cst[k]->after) TD3_RC(cst[k]->after(s));
+    const int64_t sl = cst[0]->coll_slice;
+    if (sl > 0) {                             // sharded step: replica k owns slice k (its all-gather)
+      for (int k = 0; k < n; ++k) {
+        const Group& own = coll == 0 ? hs[k]->actor : hs[k]->critic;
+        for (int j = 0; j < n; ++j) {
+          if (j == k) continue;
+          const Group& dst = coll == 0 ? hs[j]->actor : hs[j]->critic;
+          TD3_HIP(hipMemcpyAsync(dst.P + k * sl, own.P + k * sl, (size_t)sl * 4, hipMemcpyDeviceToDevice, s));
+        }
+      }
+    }
   }
   for (int k = 0; k < n; ++k) TD3_RC(ring_end_read(reinterpret_cast<Ring*>(rbs[k]), s));
   if (inject_idx || inject_noise) TD3_HIP(hipStreamSynchronize(s));

@@ -36,6 +36,7 @@ def init_rccl(policy, dist):
     dist.broadcast(t, 0)
     uid = (C.c_ubyte * 128)(*t.cpu().tolist())
     check(lib.td3_comm_init(policy._h, uid, world, rank), "td3_comm_init")
+    policy._dp_rccl = True       # optimizer state_dict() gathers the sharded moments (collective)
 
 
 def local_group(policies):

@@ -57,6 +57,7 @@ def test_launcher_starts_n_ranks_and_forwards_rank0_line(tmp_path, capfd, n):
     assert line["config"]["parallelism"] == f"dp{n}"
     assert line["value"] == pytest.approx(200.0)          # optimizer steps/s, not n x
     assert line["samples_per_s"] == pytest.approx(200.0 * 256 * n)
+    assert line["batch_gradients_per_s"] == pytest.approx(200.0 * n)
     assert line["runs"] == [200.0] * 5
     envs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
     assert [e["RANK"] for e in envs] == [str(r) for r in range(n)]

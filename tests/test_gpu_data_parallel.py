@@ -76,9 +76,14 @@ def _check_replicas_equal(pols):
             np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("name,n", [("hc_layer", 2), ("hc_layer", 4), ("hc_none", 2), ("hc_wn", 2)])
-def test_local_replicas_equal_global_batch_step(name, n):
+@pytest.mark.parametrize("name,n,shard", [("hc_layer", 2, "1"), ("hc_layer", 4, "1"), ("hc_layer", 8, "1"),
+                                          ("hc_layer", 2, "0"), ("hc_none", 2, "1"), ("hc_wn", 2, "1")])
+def test_local_replicas_equal_global_batch_step(name, n, shard, monkeypatch):
+    """shard "1" (the default): the sharded optimizer step -- replica k sums slice k, runs Adam on it
+    and hands the parameters to the others (the seam's all-gather); "0": all-reduce + replicated
+    Adam.  Adam moments are compared after the seam consolidates the owners' slices."""
     from td3_amd.data_parallel import train_local
+    monkeypatch.setenv("TD3_DP_SHARD", shard)
     G = load_golden("featured", name)
     S = featured_setup(name)
     pols, rbs = _replicas(S, n, _make)
@@ -119,8 +124,8 @@ def test_local_replicas_equal_global_batch_step(name, n):
         assert all(q._counters() == (L.total_it, L.critic_step, L.actor_step) for q in pols)
 
 
-@pytest.mark.parametrize("buckets", ["0", "1"])
-def test_c5_eight_replicas_global_batch_8192(buckets, monkeypatch):
+@pytest.mark.parametrize("buckets,shard", [("0", "1"), ("0", "0"), ("1", "1")])
+def test_c5_eight_replicas_global_batch_8192(buckets, shard, monkeypatch):
     """BASELINE config 5 (Humanoid-v4, 8 x MI355X, 1024 rows per GPU = global batch 8192) through
     the product's data-parallel stage lists: 8 replicas of one process at Humanoid widths, each on
     its 1024-row shard (split-K grad-only dW at B >= 512, the fixed-order sum in place of RCCL's
@@ -132,6 +137,7 @@ def test_c5_eight_replicas_global_batch_8192(buckets, monkeypatch):
     from helpers import featured_setup_dims
     from td3_amd.data_parallel import train_local
     monkeypatch.setenv("TD3_DP_BUCKETS", buckets)
+    monkeypatch.setenv("TD3_DP_SHARD", shard)
     n, b = 8, 1024
     S = featured_setup_dims(376, 17, 0.4, "layer", B=n * b, steps=2)
     pols, rbs = _replicas(S, n, _make)

@@ -321,13 +321,15 @@ def test_philox_noise_is_standard_normal():
     assert st.kstest(z, "norm").pvalue > 1e-4
 
 
-@pytest.mark.parametrize("name", ["hc_layer", "hc_wn"])
-def test_allreduce_path_single_rank(name):
-    """The data-parallel kernels (grad-only dW, RCCL all-reduce, flat Adam + Polyak; with weight
-    normalization the all-reduced dW feeds wn_kernel) at nranks = 1 against the oracle,
-    teacher-forced like the fused path."""
+@pytest.mark.parametrize("name,shard", [("hc_layer", "1"), ("hc_layer", "0"), ("hc_wn", "1")])
+def test_allreduce_path_single_rank(name, shard, monkeypatch):
+    """The data-parallel kernels at nranks = 1 against the oracle, teacher-forced like the fused path:
+    grad-only dW, then the sharded step (ncclReduceScatter -> flat Adam on the rank's slice ->
+    ncclAllGather -> replicated Polyak; TD3_DP_SHARD=1, the default) or RCCL all-reduce + flat Adam
+    + Polyak (0); with weight normalization the all-reduced dW feeds wn_kernel."""
     import ctypes as C
     from td3_amd import _lib
+    monkeypatch.setenv("TD3_DP_SHARD", shard)
     G = load_golden("featured", name)
     S = featured_setup(name)
     pol, rb = _make(S)
@@ -430,3 +432,43 @@ def test_large_batch_teacher_forced(B):
         _params_close(pol.critic.numpy_dict(), L.critic, L.lr, (step, "critic"))
         _params_close(pol.actor.numpy_dict(), L.actor, L.lr, (step, "actor"))
         _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (step, "critic_target"))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4])
+def test_one_launch_query_equals_launch_chain(n, monkeypatch):
+    """select_action / eval_q of n <= 4 rows as ONE act_kernel launch (in-launch H1 hand-off, head in
+    the last-arriving workgroup) against the gemv01 -> gemv -> head chain (TD3_ACT1=0) and the
+    oracle.  Layer 0's dot products are summed in another order (4-column partials, butterfly):
+    fp32 rounding apart, the same values (SURVEY §8c forward tolerance)."""
+    from td3_amd import _lib
+    S = featured_setup("hc_layer")
+    outs = []
+    st = np.random.RandomState(40 + n).standard_normal((n, S["sd"])).astype(np.float32)
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TD3_ACT1", flag)
+        pol, _ = _make(S)
+        a = pol.select_action_batch(st)
+        q = pol.eval_q_batch(st, a)
+        outs.append((a, q[0], q[1]))
+    for x, y in zip(outs[0], outs[1]):
+        np.testing.assert_allclose(x, y, rtol=1e-5, atol=1e-6)
+    ref = np.stack([orc.featured_select_action(S["actor"], S["norm"], S["ma"], x) for x in st])
+    assert _rel_to_max(outs[0][0], ref) <= 1e-5
+
+
+def test_one_launch_query_beside_training():
+    """The one-launch query's hand-off while training steps run on the learner stream (critic-only
+    steps overlap the acting stream): 60 train + select_action rounds, every action against the
+    oracle on the actor the learner holds at that moment."""
+    S = featured_setup("hc_layer")
+    pol, rb = _make(S)
+    rs = np.random.RandomState(5)
+    for it in range(60):
+        pol.train(rb, 256)
+        n = 1 + it % 4
+        st = rs.standard_normal((n, S["sd"])).astype(np.float32)
+        got = pol.select_action_batch(st) if n > 1 else pol.select_action(st[0])[None]
+        actor = pol.actor.numpy_dict()
+        ref = np.stack([orc.featured_select_action(actor, S["norm"], S["ma"], x) for x in st])
+        assert np.isfinite(got).all()
+        assert _rel_to_max(got, ref) <= 1e-5, it

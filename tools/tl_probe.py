@@ -76,7 +76,7 @@ def main():
                         print(f"   mark{k} {np.median(v[:, k] - v[:, 0]) * 0.01:5.2f}", end="")
                 print()
                 continue
-            if "gemm_kernel" not in kern and not kern.startswith("td3::dw"):
+            if "gemm_kernel" not in kern and "l0r16" not in kern and not kern.startswith("td3::dw"):
                 print(f"{name:16s} {kern[5:33]:28s} {ev:6.2f}")
                 continue
             lib.td3_tl_clear()
@@ -116,7 +116,7 @@ def main():
                               f"{np.median((v[sel, 0] - base)) * 0.01:6.2f} {(v[sel, 0] - base).max() * 0.01:6.2f}"
                               f"  dur p50/max {np.median(v[sel, 3] - v[sel, 0]) * 0.01:6.2f} "
                               f"{(v[sel, 3] - v[sel, 0]).max() * 0.01:6.2f}  end max {(v[sel, 3] - base).max() * 0.01:6.2f}")
-            if name in ("F_fwd1", "F_fwd01", "TF_fwd1", "TF_fwd01", "C_dw", "A_dw") and phase == 1:
+            if name in ("F_fwd1", "F_fwd01", "TF_fwd1", "TF_fwd01", "C_dw", "A_dw") and (phase == 1 or name == "F_fwd01"):
                 xcc = v[:, 4] & 0xFFFF
                 hw = v[:, 4] >> 32
                 print("   per-XCC wg counts:", np.bincount(xcc.astype(np.int64), minlength=8).tolist())
