@@ -62,6 +62,7 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8 TB/s spec
 # per-config rocprofv3 PMC summaries (tools/pmc_summary.py output): HBM bytes per launch per kernel
 PMC_FILES = {"halfcheetah": "pmc_traffic.json", "humanoid": "pmc_traffic_humanoid.json",
+             "pendulum": "pmc_traffic_pendulum.json",
              "particles": "pmc_traffic_particles.json"}
 FP32_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: f32 MFMA / vector peak
 

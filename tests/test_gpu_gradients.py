@@ -145,6 +145,9 @@ def test_gradients_through_adam_moments(case):
     pol.train_step(rb, S["B"], indices=idx, noise=noise)
     assert pol._counters() == (1, 1, 0)
     masks = _gpu_masks(pol, S["B"], False) if featured else None
+    if featured:        # the GPU's masks differ from the oracle's only at |z| ~ 0
+        om, near = _own_masks(L.critic, L.actor, S["norm"], S["ma"], batch[0], batch[1], False)
+        _check_mask_flips(masks, om, near, (case, "step 1"))
     L64 = _step64(L, kind, batch, noise, S["kw"], masks)
     step_fn(L, batch, noise, **kw_step(masks))
     _check(pol.critic_optimizer, L.critic_m, L.critic_v, L64.critic_m, L64.critic_v, 1, (case, "critic step 1"))
@@ -157,6 +160,9 @@ def test_gradients_through_adam_moments(case):
     pol.train_step(rb, S["B"], indices=idx, noise=noise)
     assert pol._counters() == (2, 2, 1)
     masks = _gpu_masks(pol, S["B"], True) if featured else None
+    if featured:
+        om, near = _own_masks(L.critic, L.actor, S["norm"], S["ma"], batch[0], batch[1], False)
+        _check_mask_flips({k: masks[k] for k in om}, om, near, (case, "step 2"))
     L64 = _step64(L, kind, batch, noise, S["kw"], masks)
     step_fn(L, batch, noise, **kw_step(masks))
     _check(pol.critic_optimizer, L.critic_m, L.critic_v, L64.critic_m, L64.critic_v, 2, (case, "critic step 2"))

@@ -13,7 +13,9 @@ run() {   # name "counters" bench-args
 H="--config humanoid --steps 20 --warmup 5"
 P="--config particles --steps 2 --warmup 1"
 C="--steps 40 --warmup 10"
+L="--config pendulum --steps 40 --warmup 10"
 run hf FETCH_SIZE "$H" && run hw WRITE_SIZE "$H" && run hl "TCC_HIT_sum TCC_MISS_sum" "$H" && \
 run pf FETCH_SIZE "$P" && run pw WRITE_SIZE "$P" && \
 run ps "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS" "$P" && \
-run cf FETCH_SIZE "$C" && run cw WRITE_SIZE "$C"
+run cf FETCH_SIZE "$C" && run cw WRITE_SIZE "$C" && \
+run lf FETCH_SIZE "$L" && run lw WRITE_SIZE "$L"
