@@ -213,9 +213,9 @@ int td3_comm_unique_id(unsigned char out[128]);
  * critic at B >= 512 exchanges its gradients per network, bucket 0 on a comm stream under
  * bucket 1's dW (off by default: measured slower on one rank). */
 int td3_comm_init(td3_handle* h, const unsigned char id[128], int nranks, int rank);
-/* The data-parallel optimizer step is SHARDED by default (TD3_DP_SHARD=0 in the environment when the
- * plan is built restores all-reduce + replicated Adam; weight normalization and TD3_DP_BUCKETS=1
- * keep the all-reduce): ncclReduceScatter of the gradient, Adam on this rank's 1/nranks slice,
+/* The data-parallel optimizer step is SHARDED by default for nranks > 1 (TD3_DP_SHARD in the environment
+ * when the plan is built: 0 all-reduce + replicated Adam, 2 sharded even at one rank; weight
+ * normalization and TD3_DP_BUCKETS=1 keep the all-reduce): ncclReduceScatter of the gradient, Adam on this rank's 1/nranks slice,
  * ncclAllGather of the parameters, replicated Polyak.  Parameters and targets stay identical on
  * every rank; the Adam moments of slice k live on rank k.  Reading the moments (td3_get_params
  * with TD3_*_ADAM_M / _V, e.g. a checkpoint) then needs this COLLECTIVE first, on every rank, after

@@ -2087,36 +2087,22 @@ __global__ __launch_bounds__(256) void act_kernel(ActArgs a) {
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) xr[r][jj] = a.g.xq[min(r * a.g.K0 + 4 * kg + jj, kGemvQ - 1)];
+  // layer 1's operands; layer 2's and the head's are requested after the layer-1 hand-off (in
+  // flight together with W0 they held H0 ~3 us behind the CU's ~70 GB/s L2 rate, act_tl.py)
   float w1[4][8], w2[4][8];
 #pragma unroll
   for (int j = 0; j < 4; ++j) rv_load(w1[j], P1.W + (size_t)min(o0 + j, P1.N - 1) * P1.ldw, P1.K, lane);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) rv_load(w2[j], P2.W + (size_t)min(o0 + j, P2.N - 1) * P2.ldw, P2.K, lane);
   float g1[8], bb1[8], g2[8], bb2[8], rm1[8], rm2[8];
   if (P1.lng) {
     rv_load(g1, P1.lng, P1.K, lane);
     rv_load(bb1, P1.lnb, P1.K, lane);
   }
-  if (P2.lng) {
-    rv_load(g2, P2.lng, P2.K, lane);
-    rv_load(bb2, P2.lnb, P2.K, lane);
-  }
   real_mask(rm1, P1.K, lane);
   real_mask(rm2, P2.K, lane);
   const float bia1 = gld(P1.b + min(o0 + (lane & 3), P1.N - 1));
-  const float bia2 = gld(P2.b + min(o0 + (lane & 3), P2.N - 1));
-  // the head's weights (any workgroup may arrive last): rows 0..7 of W4, LN2 affine, biases; a
-  // head of more outputs loads the rest in its loop (in the loop, each row was a dependent round trip)
   const HeadProb& H = a.head[k];
   constexpr int kPre = 8;
   float w4[kPre][8], hg[8], hb[8];
-#pragma unroll
-  for (int o = 0; o < kPre; ++o) rv_load(w4[o], H.W4 + (size_t)min(o, H.nout - 1) * H.ldw, H.ldw, lane);
-  if (H.lng) {
-    rv_load(hg, H.lng, H.ldh, lane);
-    rv_load(hb, H.lnb, H.ldh, lane);
-  }
-  const float b4 = lane < H.nout ? gld(H.b4 + lane) : 0.f;
   // 1. H0 of every query row: 4-column partial dot products, summed over the TPR threads of a row
   //    (butterfly), + b0, ReLU; rows past N0 are zero
 #pragma unroll
@@ -2166,8 +2152,24 @@ __global__ __launch_bounds__(256) void act_kernel(ActArgs a) {
   __syncthreads();
   TL_MARK(6);
   const int nb = (int)gridDim.x;
+  if (threadIdx.x == 0) __hip_atomic_fetch_add((GAS int*)c1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // layer 2's operands and the head's (any workgroup may arrive last: rows 0..7 of W4, LN2 affine,
+  // biases; a head of more outputs loads the rest in its loop), in flight during the poll
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rv_load(w2[j], P2.W + (size_t)min(o0 + j, P2.N - 1) * P2.ldw, P2.K, lane);
+  if (P2.lng) {
+    rv_load(g2, P2.lng, P2.K, lane);
+    rv_load(bb2, P2.lnb, P2.K, lane);
+  }
+  const float bia2 = gld(P2.b + min(o0 + (lane & 3), P2.N - 1));
+#pragma unroll
+  for (int o = 0; o < kPre; ++o) rv_load(w4[o], H.W4 + (size_t)min(o, H.nout - 1) * H.ldw, H.ldw, lane);
+  if (H.lng) {
+    rv_load(hg, H.lng, H.ldh, lane);
+    rv_load(hb, H.lnb, H.ldh, lane);
+  }
+  const float b4 = lane < H.nout ? gld(H.b4 + lane) : 0.f;
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((GAS int*)c1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     for (int spin = 0; __hip_atomic_load((GAS int*)c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nb; ++spin) {
       if (spin > (1 << 22)) {

@@ -952,11 +952,14 @@ static bool dp_overlap(const td3_handle* h) {
 }
 
 // The data-parallel optimizer step: sharded (reduce-scatter -> Adam on the rank's 1/N slice ->
-// all-gather of the parameters; TD3_DP_SHARD=1, the default) or all-reduce -> replicated flat Adam
-// (0).  Weight normalization and the bucketed schedule keep the all-reduce.  Read at plan build.
+// all-gather of the parameters) or all-reduce -> replicated flat Adam.  TD3_DP_SHARD = 1 (default):
+// sharded for more than one rank -- at one rank the two are the same computation and the
+// all-reduce form is one RCCL launch and one Polyak pass cheaper (bench.py --dp-self);
+// 2: sharded always (tests, pricing); 0: all-reduce.  Weight normalization and the bucketed
+// schedule keep the all-reduce.  Read at plan build.
 static bool dp_shard(const td3_handle* h) {
-  (void)h;
-  return env_int("TD3_DP_SHARD", 1) != 0;
+  const int m = env_int("TD3_DP_SHARD", 1);
+  return m == 2 || (m == 1 && h->nranks > 1);
 }
 static int64_t shard_slice(const Group& g, int nranks) { return ((g.size + 4 * nranks - 1) / (4 * nranks)) * 4; }
 

@@ -321,12 +321,13 @@ def test_philox_noise_is_standard_normal():
     assert st.kstest(z, "norm").pvalue > 1e-4
 
 
-@pytest.mark.parametrize("name,shard", [("hc_layer", "1"), ("hc_layer", "0"), ("hc_wn", "1")])
+@pytest.mark.parametrize("name,shard", [("hc_layer", "2"), ("hc_layer", "0"), ("hc_wn", "2")])
 def test_allreduce_path_single_rank(name, shard, monkeypatch):
     """The data-parallel kernels at nranks = 1 against the oracle, teacher-forced like the fused path:
     grad-only dW, then the sharded step (ncclReduceScatter -> flat Adam on the rank's slice ->
-    ncclAllGather -> replicated Polyak; TD3_DP_SHARD=1, the default) or RCCL all-reduce + flat Adam
-    + Polyak (0); with weight normalization the all-reduced dW feeds wn_kernel."""
+    ncclAllGather -> replicated Polyak; TD3_DP_SHARD=2 forces it at one rank, where the default
+    runs the all-reduce form) or RCCL all-reduce + flat Adam + Polyak (0); with weight
+    normalization the all-reduced dW feeds wn_kernel."""
     import ctypes as C
     from td3_amd import _lib
     monkeypatch.setenv("TD3_DP_SHARD", shard)
