@@ -281,10 +281,6 @@ int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int 
 int launch_l0r16(int nct, int wk, int gather, const GemmTable& t, int nblocks, int Bp, Counters* bump,
                  int bump_actor, hipStream_t s);
 int l0r16_lds_bytes(int Kp, int nct, int wk);
-// (2, 4) l0r16 tiles + a gemm_body stage in one launch (instantiated second stages: l0r16_dual_supported)
-int l0r16_dual_supported(int m2, int w2, int p2);
-int launch_l0r16_dual(const GemmTable& t1, int nb1, int m2, int w2, int p2, const GemmTable& t2, int nb2, int Bp,
-                      int lds, hipStream_t s);
 // Two independent GEMM stages in one launch (stage 2's tile ids follow stage 1's); only the pairs
 // gemm2_supported() reports are instantiated.
 int gemm2_supported(int m1, int w1, int p1, int m2, int w2, int p2);

@@ -1636,10 +1636,15 @@ __global__ __launch_bounds__(64 * kNW, (W1 == 4 || W2 == 4) ? 4 : (W1 == kWn4x2 
 constexpr int kR16XS = 36;      // LDS row stride of the staged 16 input rows
 
 template <int NCT, int WK, bool GATHER>
-__device__ __forceinline__ void l0r16_body(int b, int nprob, int tb1, int tb2, int tb3, int Bp, const GemmTable& tab,
-                                           Counters* bump, int bump_actor, float* smem) {
+__global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
+                                                              GemmTable tab, Counters* bump, int bump_actor) {
   constexpr int NW = NCT * WK, NT = 64 * NW, OUTW = 16 * NCT;
   static_assert(NW >= 8 && NW <= 16 && NT % OUTW == 0, "l0r16: 8 .. 16 waves, whole output rows per pass");
+  extern __shared__ float4 smem4[];
+  float* smem = reinterpret_cast<float*>(smem4);
+  const int b = xcd_tile(nb);
+  TL_MARK(0);
+  if (b >= nb) return;
   int pi = 0;
   if (nprob > 1 && b >= tb1) pi = 1;
   if (nprob > 2 && b >= tb2) pi = 2;
@@ -1873,41 +1878,6 @@ __device__ __forceinline__ void l0r16_body(int b, int nprob, int tb1, int tb2, i
       bump->pw[2] *= bump->beta[2];
       bump->pw[3] *= bump->beta[3];
     }
-  }
-}
-
-template <int NCT, int WK, bool GATHER>
-__global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
-                                                              GemmTable tab, Counters* bump, int bump_actor) {
-  extern __shared__ float4 smem4[];
-  const int b = xcd_tile(nb);
-  TL_MARK(0);
-  if (b >= nb) return;
-  l0r16_body<NCT, WK, GATHER>(b, nprob, tb1, tb2, tb3, Bp, tab, bump, bump_actor, reinterpret_cast<float*>(smem4));
-}
-
-// The fused layer-0 stage on 16-row tiles beside an input-grad stage in one launch (gemm2_kernel's
-// dual form: the target twin's TF_fwd01 with the unit backward's CB_bwd2): the l0r16 tiles take the
-// first workgroup ids, dealt over the XCDs as xcd_tile does, the gemm_body tiles follow; 8 waves
-// each, two workgroups per CU (<= 128 VGPRs) so the second stage fills what the first leaves.
-template <int NCT, int WK, int M2, int W2, int P2>
-__global__ __launch_bounds__(64 * NCT * WK, 4) void l0r16_dual_kernel(int nb1, int nb2, int Bp, int np1, int a1, int a2,
-                                                                      int a3, int np2, int c1, int c2, int c3,
-                                                                      GemmTable t1, GemmTable t2) {
-  static_assert(NCT * WK == kNW, "dual launch: both bodies run kNW waves");
-  extern __shared__ float4 smem4[];
-  TL_MARK(0);
-  const int per1 = (nb1 + 7) >> 3, per2 = (nb2 + 7) >> 3;
-  float* smem = reinterpret_cast<float*>(smem4);
-  const int id = (int)blockIdx.x;
-  if (id < 8 * per1) {
-    const int b = (id & 7) * per1 + (id >> 3);
-    if (b >= nb1) return;
-    l0r16_body<NCT, WK, false>(b, np1, a1, a2, a3, Bp, t1, nullptr, 0, smem);
-  } else {
-    const int l = id - 8 * per1, b = (l & 7) * per2 + (l >> 3);
-    if (b >= nb2) return;
-    gemm_body<M2, W2, P2>(b, np2, c1, c2, c3, Bp, t2, nullptr, 0, smem);
   }
 }
 
@@ -3578,37 +3548,6 @@ int launch_l0r16(int nct, int wk, int gather, const GemmTable& t, int nblocks, i
   return 0;
 }
 
-#define TD3_L0R16_DUAL_PAIRS(X) X(1, 1, kProCopy) X(1, 0, kProCopy) X(1, 4, kProCopy)
-int l0r16_dual_supported(int m2, int w2, int p2) {
-#define TD3_L0D_Q(A, B, C) \
-  if (m2 == A && w2 == B && p2 == C) return 1;
-  TD3_L0R16_DUAL_PAIRS(TD3_L0D_Q)
-#undef TD3_L0D_Q
-  return 0;
-}
-int launch_l0r16_dual(const GemmTable& t1, int nb1, int m2, int w2, int p2, const GemmTable& t2, int nb2, int Bp,
-                      int lds, hipStream_t s) {
-  const dim3 grid(8 * (((nb1 + 7) >> 3) + ((nb2 + 7) >> 3)));
-  auto dir = [](const GemmTable& t, int n, int i) { return t.nprob > i ? t.p[i].tile_begin : n; };
-  const int l = std::max(lds, l0r16_lds_bytes(512, 2, 4));
-  bool done = false;
-#define TD3_L0D_L(A, B, C)                                                                                   \
-  if (!done && m2 == A && w2 == B && p2 == C) {                                                              \
-    hipLaunchKernelGGL((l0r16_dual_kernel<2, 4, A, B, C>), grid, dim3(64 * kNW), l, s, nb1, nb2, Bp, t1.nprob, \
-                       dir(t1, nb1, 1), dir(t1, nb1, 2), dir(t1, nb1, 3), t2.nprob, dir(t2, nb2, 1), dir(t2, nb2, 2), \
-                       dir(t2, nb2, 3), t1, t2);                                                             \
-    done = true;                                                                                             \
-  }
-  TD3_L0R16_DUAL_PAIRS(TD3_L0D_L)
-#undef TD3_L0D_L
-  if (!done) {
-    set_error("launch_l0r16_dual: second stage (%d,%d,%d) not instantiated", m2, w2, p2);
-    return -1;
-  }
-  TD3_HIP(hipGetLastError());
-  return 0;
-}
-
 int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int Bp, int lds,
                 Counters* bump, int bump_actor, hipStream_t s) {
   if (nblocks <= 0) return 0;
@@ -3899,10 +3838,7 @@ int kernels_init() {
                         (const void*)gemm_kernel<1, kWn4x2, kProCopy>, (const void*)gemm_kernel<1, kWn4x2, kProLNBwd>,
                         (const void*)gemm_kernel<1, kWn4x2, kProHeadBwd>,
                         (const void*)l0r16_kernel<5, 2, true>, (const void*)l0r16_kernel<5, 2, false>,
-                        (const void*)l0r16_kernel<2, 4, true>, (const void*)l0r16_kernel<2, 4, false>,
-                        (const void*)l0r16_dual_kernel<2, 4, 1, 1, kProCopy>,
-                        (const void*)l0r16_dual_kernel<2, 4, 1, 0, kProCopy>,
-                        (const void*)l0r16_dual_kernel<2, 4, 1, 4, kProCopy>})
+                        (const void*)l0r16_kernel<2, 4, true>, (const void*)l0r16_kernel<2, 4, false>})
     TD3_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   return 0;
 }

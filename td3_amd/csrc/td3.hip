@@ -178,7 +178,6 @@ struct Scratch {
 };
 
 // A GEMM stage's launch, kept so the planner can merge two independent stages into one launch.
-constexpr int kWnL0R16 = -2;     // GemmLaunch::wn of a (2, 4) l0r16 stage (launch_l0r16_dual pairs it)
 struct GemmLaunch {
   int mode, wn, pro;
   GemmTable t;
@@ -493,22 +492,6 @@ static bool merge_gemm_pair(std::vector<Stage>& st, size_t i, size_t j) {
   if (!a0 || !b0 || !a0->plain || !b0->plain || a0->Bp != b0->Bp) return false;
   const bool a_first = a0->mode == 0;
   const GemmLaunch f = a_first ? *a0 : *b0, g = a_first ? *b0 : *a0;
-  if (f.wn == kWnL0R16 || g.wn == kWnL0R16) {       // l0r16 tiles (2, 4) beside an input-grad stage
-    if (f.wn != kWnL0R16 || g.mode != 1 || !l0r16_dual_supported(g.mode, g.wn, g.pro)) return false;
-    Stage m;
-    m.name = st[i].name + "+" + st[j].name;
-    m.flops = st[i].flops + st[j].flops;
-    char kname[96];
-    snprintf(kname, sizeof(kname), "td3::l0r16_dual_kernel<2, 4, %d, %d, %d>", g.mode, g.wn, g.pro);
-    m.kernel = kname;
-    const int lds = std::max(f.lds, g.lds);
-    m.run = [=](hipStream_t s) {
-      return launch_l0r16_dual(f.t, f.blocks, g.mode, g.wn, g.pro, g.t, g.blocks, f.Bp, lds, s);
-    };
-    st[i] = m;
-    st.erase(st.begin() + (long)j);
-    return true;
-  }
   if (!gemm2_supported(f.mode, f.wn, f.pro, g.mode, g.wn, g.pro)) return false;
   Stage m;
   m.name = st[i].name + "+" + st[j].name;
@@ -636,17 +619,9 @@ static bool can_fuse_l0(const std::vector<FwdItem>& items) {
 // 80-column workgroups (10 waves) when 16-row x 80-column tiles of every network fit 256 workgroups
 // and 32-column ones (8 waves) would not, else 32-column workgroups when those fit (one network:
 // AF_fwd01), else none (the 32-row gemm_body stage).  B < 512 only; TD3_L0R16=0 turns it off.
-static bool l0r16_config(const std::vector<FwdItem>& items, int Bp, int* nct, int* wk, bool pair = false) {
+static bool l0r16_config(const std::vector<FwdItem>& items, int Bp, int* nct, int* wk) {
   static const bool on = env_int("TD3_L0R16", 1) != 0;
   if (!on || Bp >= 512 || Bp % 16) return false;
-  if (pair) {                 // a stage for a dual launch: the 8-wave (2, 4) form
-    static const bool pon = env_int("TD3_L0R16_PAIR", 1) != 0;
-    for (auto& it : items)
-      if (it.net->lin[1].Kp > 512 || it.net->lin[0].Np != it.net->lin[1].Kp) return false;
-    *nct = 2;
-    *wk = 4;
-    return pon;
-  }
   int b80 = 0, b32 = 0;
   for (auto& it : items) {
     const LinearL& L = it.net->lin[1];
@@ -670,8 +645,7 @@ static bool l0r16_config(const std::vector<FwdItem>& items, int Bp, int* nct, in
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
                           Counters* bump, int bump_actor, const RingSide* ring = nullptr,
-                          const RingOut* ro = nullptr, int o_r = 0, bool fuse_l0 = false, bool r16 = false,
-                          bool r16_pair = false) {
+                          const RingOut* ro = nullptr, int o_r = 0, bool fuse_l0 = false, bool r16 = false) {
   const bool norm = h->cfg.norm == 1;
   fuse_l0 = fuse_l0 && can_fuse_l0(items);
   for (int l = fuse_l0 ? 1 : 0; l < 3; ++l) {
@@ -789,7 +763,7 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
     // the step counters are bumped by the launch after the one that draws the sample
     const int bump_l = fuse_l0 ? 2 : 1;
     int nct = 0, wk = 0;
-    if (l0 && r16 && l0r16_config(items, Bp, &nct, &wk, r16_pair && !gather)) {
+    if (l0 && r16 && l0r16_config(items, Bp, &nct, &wk)) {
       // the same problems on 16-row tiles of 16*nct real layer-1 columns (the pad columns of H1 are
       // zero from the scratch's creation and no stage writes them)
       int nb16 = 0;
@@ -823,9 +797,6 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       } else {
         st.push_back({name, [=](hipStream_t s) { return launch_l0r16(nct, wk, 0, t, nb16, Bp, bmp, bump_actor, s); },
                       flops, kname});
-        if (r16_pair && nct == 2 && wk == 4 && !bmp)      // mergeable into a dual launch (merge_gemm_pair)
-          st.back().gemm = std::make_shared<GemmLaunch>(
-              GemmLaunch{0, kWnL0R16, pro, t, nb16, Bp, l0r16_lds_bytes(512, 2, 4), true});
       }
       continue;
     }
@@ -1597,7 +1568,7 @@ static int build_step(td3_handle* h, int B) {
         }
         TD3_RC(add_bwd_stages(h, P->tables, st, cb, Bp, B, "CB", true, false, &rows));
         std::vector<FwdItem> f2 = {{&q1, Ptq1, &P->TQ[0], false, false}, {&q2, Ptq2, &P->TQ[1], false, false}};
-        TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, nullptr, nullptr, 0, true, true, true));
+        TD3_RC(add_fwd_stages(h, P->tables, st, f2, Bp, B, "TF", nullptr, 0, nullptr, nullptr, 0, true));
         {   // the unit backward's input-grad stages share launches with the target twin's layers, in
             // order: TF layer k moves up to CB stage k only while every earlier TF layer moved too
           const char* cbn[2] = {"CB_bwd2", "CB_bwd1"};
