@@ -192,6 +192,8 @@ struct ActArgs {
   float max_action;
   unsigned* flag;                       // nullable: [network] = seq once its outputs are written
   unsigned seq;                         //   (mapped host memory: the host polls it, no stream sync)
+  float* part;                          // nullable: act2_kernel's partial slab [network][nb][part_ld]
+  int part_ld, part_n2;                 //   (floats per workgroup >= (B' + 2) * part_n2 + 8; part_n2 >= N2)
 };
 int launch_act(const ActArgs& a, int nprob, hipStream_t s);
 

@@ -629,12 +629,13 @@ static bool l0r16_config(const std::vector<FwdItem>& items, int Bp, int* nct, in
     b80 += (Bp / 16) * ((L.N + 79) / 80);
     b32 += (Bp / 16) * ((L.N + 31) / 32);
   }
+  static const int maxwg = env_int("TD3_L0R16_MAXWG", 256);
   if (b32 <= 256) {
     *nct = 2;
     *wk = 4;
     return true;
   }
-  if (b80 <= 256) {
+  if (b80 <= maxwg) {
     *nct = 5;
     *wk = 2;
     return true;
@@ -2507,6 +2508,20 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     float* oq[2] = {A->q[0], A->q[1]};
     A->act1 = A->hio && mk(A->a1_act, A->g01_act, A->gv_act[2], {&an}, h->actor.P, ea, oa, A->ldo, kHeadPolicy, ctr) &&
               mk(A->a1_q, A->g01_q, A->gv_q[2], {&q1, &q2}, h->critic.P, eq, oq, 1, kHeadQ, ctr + 8);
+    if (A->act1 && env_int("TD3_ACT1", 1) == 2) {     // one-hand-off form: the partial slab
+      const int n2p = std::max(pad32(an.lin[2].N), pad32(q1.lin[2].N));
+      const int ld = 6 * n2p + 8;                       // up to kGemvRows = 4 rows
+      const int nb = std::max((an.lin[1].N + 15) / 16, (q1.lin[1].N + 15) / 16);
+      float* slab = nullptr;
+      TD3_HIP(hipMalloc(&slab, (size_t)2 * 2 * nb * ld * sizeof(float)));   // act and eval_q, 2 networks
+      A->tables.push_back(slab);
+      A->a1_act.part = slab;
+      A->a1_q.part = slab + (size_t)2 * nb * ld;
+      for (ActArgs* x : {&A->a1_act, &A->a1_q}) {
+        x->part_ld = ld;
+        x->part_n2 = n2p;
+      }
+    }
     if (A->act1) {       // completion flags in the mapped block (io_floats reserves 4 * 64 floats of slack)
       float* hf = nullptr;
       A->a1_act.flag = reinterpret_cast<unsigned*>(io.take(64, &hf));
