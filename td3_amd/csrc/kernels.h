@@ -77,7 +77,7 @@ constexpr int gemm_nw(int mode, int wn, int pro) {
 constexpr int kMaxEx = 24;
 
 struct GemmProb {
-  // The first 128 bytes (pointers, then ints, no implicit padding) are everything a GEMM
+  // The first 136 bytes (pointers, then ints, no implicit padding) are everything a GEMM
   // workgroup reads before its operand loads: gemm_kernel requests all of them in one scalar batch.
   const float* A;                 // batch rows of the A side (kProCopy / kProLN / kProLNBwd)
   const float* lng; const float* lnb;   // LayerNorm affine of the A-side features
@@ -99,7 +99,13 @@ struct GemmProb {
   int tile_begin;                 // first flat workgroup id of this problem (row kernels: unused)
   int norm;                       // LayerNorm present (norm="layer")
   int B;                          // real batch rows (rows >= B are padding)
-  int hot_pad;
+  // MODE 0 weight image: the 16-B piece W[n][4j .. 4j+3] is at W + n * ldw + j * wsk.  Row-major
+  // [n][Kp] (the parameter arena): ldw = Kp, wsk = 4 (0 reads as 4).  The k-quad image [Kp/4][Np][4]
+  // (td3.hip Group::P4 / T4): ldw = 4, wsk = 4 * Np -- the 16 lanes of an MFMA fragment load (16 or 32
+  // consecutive n, one k-quad) read 256 contiguous bytes instead of 16 rows' pieces.
+  int wsk;
+  int w0sk;                       // kProL0*: the same for W0 (ex[8]): 0 = row-major [N0p][32]
+  int wpad_;
   // head-prologue operands (meaning per kind: see the prologue functions in kernels.hip)
   float* ex[kMaxEx];
   int exi[12];
@@ -192,8 +198,6 @@ struct ActArgs {
   float max_action;
   unsigned* flag;                       // nullable: [network] = seq once its outputs are written
   unsigned seq;                         //   (mapped host memory: the host polls it, no stream sync)
-  float* part;                          // nullable: act2_kernel's partial slab [network][nb][part_ld]
-  int part_ld, part_n2;                 //   (floats per workgroup >= (B' + 2) * part_n2 + 8; part_n2 >= N2)
 };
 int launch_act(const ActArgs& a, int nprob, hipStream_t s);
 
@@ -229,6 +233,9 @@ enum DwMode : int { kDwGrad = 0, kDwAdam = 1, kDwAdamPolyak = 2 };
 
 struct AdamArgs {
   float* P; float* G; float* M; float* V; float* T;   // group arenas
+  // nullable: the k-quad images of P / T (GemmProb::wsk) that the forward GEMM stages read; dw_kernel
+  // writes every updated weight element to them too (td3.hip Group::P4 / T4)
+  float* P4; float* T4;
   const Counters* ctr; int which;                     // 0: critic_step, 1: actor_step
   double lr, beta1, beta2, eps;
   float tau;
@@ -326,6 +333,15 @@ struct WnArgs {
 enum WnMode : int { kWnDerive = 0, kWnAdam = 1 };
 int launch_wn(const WnArgs& a, hipStream_t s);
 int launch_polyak_flat(float* T, const float* P, int64_t n, float tau, hipStream_t s);
+// k-quad weight images (GemmProb::wsk): dst[off + ((k/4) * Np + n) * 4 + k % 4] = src[off + n * Kp + k]
+// for every listed matrix (off, Np, Kp), over up to two (src, dst) arena pairs (P -> P4, T -> T4)
+constexpr int kMaxW4Mats = 16;
+struct W4PackArgs {
+  const float* src[2]; float* dst[2]; int npair;
+  int64_t off[kMaxW4Mats]; int Np[kMaxW4Mats], Kp[kMaxW4Mats]; int64_t first[kMaxW4Mats + 1];   // piece ranges
+  int nmat;
+};
+int launch_w4_pack(const W4PackArgs& a, hipStream_t s);
 int kernels_init();
 
 }  // namespace td3

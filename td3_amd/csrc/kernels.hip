@@ -1173,14 +1173,25 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_kernel2(int Bp, int n1, Ge
 // With kNW waves, a wave holds at most 16 / kNW chunks of K <= 512 (WN = 1: WK = kNW;
 // WN = 4 only runs K <= 128 with WK = kNW / 4).
 
+// The k-quad stride of a MODE 0 weight image (GemmProb::wsk; 0: row-major)
+__device__ __forceinline__ int w_sk(int wsk) { return wsk ? wsk : 4; }
+// W0 of the fused layer-0 stages (ex[8]): row stride and k-quad stride (GemmProb::w0sk)
+__device__ __forceinline__ int w0_sn(int w0sk) { return w0sk ? 4 : 32; }
+__device__ __forceinline__ int w0_sk(int w0sk) { return w0sk ? w0sk : 4; }
+
 template <int MODE>
 __device__ __forceinline__ void load_chunk(const GemmProb& P, float (&b)[16], int ch, int ncol, int h) {
   const int kb = ch * 32 + 16 * h;
   if (MODE == 0) {
-    const float* wp = P.W + (size_t)ncol * P.ldw + kb;
+    const int sk = w_sk(P.wsk);
+    const float* wp = P.W + (size_t)ncol * P.ldw + (size_t)(kb >> 2) * sk;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 v = gld4(wp + 4 * q);
+#ifdef TD3_KO_GEMM    // knockout experiment (wrong results): no weight loads
+      const float4 v = make_float4(1e-3f * q, 2e-3f * kb, 3e-3f, 4e-3f * ncol);
+#else
+      const float4 v = gld4(wp + (size_t)q * sk);
+#endif
       b[4 * q + 0] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
     }
   } else {
@@ -1203,10 +1214,15 @@ template <int MODE>
 __device__ __forceinline__ void load_chunk16(const GemmProb& P, float (&b)[16], int ch, int ncol, int g) {
   const int kb = ch * 32 + 8 * g;
   if (MODE == 0) {
-    const float* wp = P.W + (size_t)ncol * P.ldw + kb;
+    const int sk = w_sk(P.wsk);
+    const float* wp = P.W + (size_t)ncol * P.ldw + (size_t)(kb >> 2) * sk;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const float4 v = gld4(wp + 4 * q);
+#ifdef TD3_KO_GEMM
+      const float4 v = make_float4(1e-3f * q, 2e-3f * kb, 3e-3f, 4e-3f * ncol);
+#else
+      const float4 v = gld4(wp + (size_t)q * sk);
+#endif
       b[4 * q + 0] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
     }
   } else {
@@ -1279,11 +1295,11 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
       asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
                    "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
                    "s"(P.norm), "s"(P.B), "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.seed),
-                   "s"(tab.rs.ctr), "s"(P.exi[0]), "s"(P.exi[1]));
+                   "s"(tab.rs.ctr), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.wsk), "s"(P.w0sk));
     else
       asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
                    "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
-                   "s"(P.norm), "s"(P.B));
+                   "s"(P.norm), "s"(P.B), "s"(P.wsk), "s"(P.w0sk));
   } else {
     if constexpr (PRO == kProHeadBwd)      // one batch with the head operands (a second asm would be a
       asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.W), "s"(P.C), "s"(P.lda), "s"(P.Kreal),
@@ -1292,7 +1308,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
     else                                   // second dependent kernel-argument round trip)
       asm volatile("" ::"s"(P.A), "s"(P.lng), "s"(P.lnb), "s"(P.H), "s"(P.stats), "s"(P.Aout), "s"(P.W), "s"(P.bias),
                    "s"(P.C), "s"(P.lda), "s"(P.Kreal), "s"(P.Kp), "s"(P.ldh), "s"(P.ldao), "s"(P.ldw), "s"(P.Nout),
-                   "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.hot_pad));
+                   "s"(P.ldc), "s"(P.relu), "s"(P.ntiles), "s"(P.tile_begin), "s"(P.norm), "s"(P.B), "s"(P.wsk));
     if constexpr (PRO == kProGather)
       asm volatile("" ::"s"(P.ex[0]), "s"(P.ex[1]), "s"(P.ex[2]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[3]),
                    "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.idx_out), "s"(tab.rs.seed),
@@ -1332,13 +1348,18 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
   float w0[2][16], b0v[2];
   if constexpr (kL0) {
     const int koff = l0_koff(P, h);
+    const int sn0 = w0_sn(P.w0sk), sk0 = w0_sk(P.w0sk);
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       const int tile = min(wave + kNW * ct, (P.exi[5] >> 5) - 1);
-      const float* wp = P.ex[8] + (size_t)(tile * 32 + i) * 32 + koff;
+      const float* wp = P.ex[8] + (size_t)(tile * 32 + i) * sn0 + (size_t)(koff >> 2) * sk0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = gld4(wp + 4 * q);
+#ifdef TD3_KO_GEMM
+        const float4 v = make_float4(1e-3f * q, 2e-3f * tile, 3e-3f, 4e-3f * i);
+#else
+        const float4 v = gld4(wp + (size_t)q * sk0);
+#endif
         w0[ct][4 * q + 0] = v.x; w0[ct][4 * q + 1] = v.y; w0[ct][4 * q + 2] = v.z; w0[ct][4 * q + 3] = v.w;
       }
       b0v[ct] = gld(P.ex[9] + tile * 32 + i);
@@ -1552,7 +1573,7 @@ __device__ __forceinline__ void gemm_body(int b, int nprob, int tb1, int tb2, in
       const int tcol = P.exi[10], tn = P.exi[11];
       for (int e = threadIdx.x; e < OUTW * tn; e += NT) {
         const int r = e / tn, o = e % tn, n = n0 + r;
-        if (r % mtiles == mt && n < P.Nout) gst(tc + ((size_t)o * P.Nout + n), gld(P.W + ((size_t)n * P.ldw + tcol + o)));
+        if (r % mtiles == mt && n < P.Nout) gst(tc + ((size_t)o * P.Nout + n), gld(P.W + ((size_t)n * P.ldw + (size_t)((tcol + o) >> 2) * w_sk(P.wsk) + ((tcol + o) & 3))));
       }
     }
   }
@@ -1655,11 +1676,11 @@ __global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob,
     asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
                  "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
                  "s"(P.norm), "s"(P.B), "s"(tab.rs.data), "s"(tab.rs.rec), "s"(tab.rs.d_size), "s"(tab.rs.seed),
-                 "s"(tab.rs.ctr), "s"(P.exi[0]), "s"(P.exi[1]));
+                 "s"(tab.rs.ctr), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.wsk), "s"(P.w0sk));
   else
     asm volatile("" ::"s"(P.A), "s"(P.lda), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.W),
                  "s"(P.ldw), "s"(P.Kp), "s"(P.lng), "s"(P.lnb), "s"(P.bias), "s"(P.Nout), "s"(P.tile_begin),
-                 "s"(P.norm), "s"(P.B));
+                 "s"(P.norm), "s"(P.B), "s"(P.wsk), "s"(P.w0sk));
   const int mtiles = Bp >> 4;
   const int t = b - P.tile_begin;
   const int mt = t % mtiles, nt = t / mtiles;
@@ -1701,8 +1722,12 @@ __global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob,
 #pragma unroll
   for (int q = 0; q < kQ0; ++q) {
     const int tau = min(wave + NW * q, n0t - 1);
-    const float* wp = P.ex[8] + (size_t)(tau * 16 + j16) * 32 + 8 * g;
-    const float4 u = gld4(wp), v = gld4(wp + 4);
+    const float* wp = P.ex[8] + (size_t)(tau * 16 + j16) * w0_sn(P.w0sk) + (size_t)(2 * g) * w0_sk(P.w0sk);
+#ifdef TD3_KO_W0      // knockout experiment (wrong results): no layer-0 weight loads
+    const float4 u = make_float4(1e-3f * q, 2e-3f, 3e-3f, 4e-3f * j16), v = u;
+#else
+    const float4 u = gld4(wp), v = gld4(wp + w0_sk(P.w0sk));
+#endif
     w0[q][0] = u.x; w0[q][1] = u.y; w0[q][2] = u.z; w0[q][3] = u.w;
     w0[q][4] = v.x; w0[q][5] = v.y; w0[q][6] = v.z; w0[q][7] = v.w;
     b0v[q] = gld(P.ex[9] + tau * 16 + j16);
@@ -1725,8 +1750,13 @@ __global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob,
 #pragma unroll
     for (int q = 0; q < kMaxCh; ++q) {
       const int ch = min(cb + q, ce - 1);
-      const float* wp = P.W + (size_t)wrow * P.ldw + ch * 32 + 8 * g;
-      const float4 u = gld4(wp), v = gld4(wp + 4);
+      const int sk = w_sk(P.wsk);
+      const float* wp = P.W + (size_t)wrow * P.ldw + (size_t)(ch * 8 + 2 * g) * sk;
+#ifdef TD3_KO_W1      // knockout experiment (wrong results): no layer-1 weight loads
+      const float4 u = make_float4(1e-3f * ch, 2e-3f, 3e-3f, 4e-3f * j16), v = u;
+#else
+      const float4 u = gld4(wp), v = gld4(wp + sk);
+#endif
       bw[q][0] = u.x; bw[q][1] = u.y; bw[q][2] = u.z; bw[q][3] = u.w;
       bw[q][4] = v.x; bw[q][5] = v.y; bw[q][6] = v.z; bw[q][7] = v.w;
     }
@@ -2254,266 +2284,6 @@ __global__ __launch_bounds__(256) void act_kernel(ActArgs a) {
   TL_MARK(3);
 }
 
-// The query with ONE in-launch hand-off (act2_kernel, TD3_ACT1=2): layer 2 is linear in the LN1
-// output, so each workgroup turns its 16 layer-1 columns (k-slice of layer 2) into partial sums
-//   A[r][o] = sum_c W2[o][c] g1_c h[r][c],  C[o] = sum_c W2[o][c] g1_c,  D[o] = sum_c W2[o][c] b1_c
-// plus the slice's LayerNorm statistics (count, mean, M2), and the LAST arriver sums the partials in
-// workgroup order (bitwise reproducible), merges the statistics (Chan et al.), and forms
-//   z2[r][o] = rstd_r (A[r][o] - mean_r C[o]) + D[o] + b2[o]
-// = W2 . LN1(h1[r]) + b2 (TD3_featured.py:41-46: Linear -> ReLU -> LayerNorm), then LN2 and the
-// head.  One drain / counter / reload instead of two (act_kernel: 2-3 us each, tools/act_tl.py).
-template <int R, int KQ>
-__global__ __launch_bounds__(256) void act2_kernel(ActArgs a) {
-  __shared__ float h0[R][512];
-  __shared__ float s_h1[R][16];
-  __shared__ float s_h2[R][512];
-  __shared__ float s_st[R][2];
-  __shared__ int s_flag;
-  TL_MARK(0);
-  const int k = blockIdx.y;
-  const GemvProb& P1 = a.g.l1.p[k];
-  const GemvProb& P2 = a.l2[k];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int B = a.g.l1.B;
-  const int nb = (int)gridDim.x;
-  const int k0 = blockIdx.x * 16;                       // this workgroup's layer-1 columns / layer-2 k-slice
-  const int o0 = k0 + wave * 4;                         // this wave's 4 layer-1 columns
-  const int nk = min(16, P1.N - k0);                    // real columns of the slice
-  int* c1 = a.ctr + 2 * k;
-  float* part = a.part + (size_t)k * nb * a.part_ld;    // [nb][part_ld]: A[R][N2p], C[N2p], D[N2p], st[R][2]
-  const int N2p = a.part_n2;
-  // layer 0's weights first (coalesced rows, as act_kernel)
-  const float* W0 = a.g.W0[k];
-  const float* b0 = a.g.b0[k];
-  constexpr int LW = 4 * KQ;
-  constexpr int TPR = LW / 4, RPP = 256 / TPR, NPASS = 512 / RPP;
-  const int kg = threadIdx.x % TPR, rsub = threadIdx.x / TPR;
-  float4 w0r[NPASS];
-  float b0r[NPASS];
-#pragma unroll
-  for (int i = 0; i < NPASS; ++i) {
-    const int o = min(rsub + RPP * i, a.g.N0 - 1);
-    w0r[i] = gld4(W0 + (size_t)o * LW + 4 * kg);
-    b0r[i] = gld(b0 + o);
-  }
-  float xr[R][4];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) xr[r][jj] = a.g.xq[min(r * a.g.K0 + 4 * kg + jj, kGemvQ - 1)];
-  // layer 1: 4 rows per wave, LN0 affine, biases
-  float w1[4][8], g1[8], bb1[8], rm1[8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) rv_load(w1[j], P1.W + (size_t)min(o0 + j, P1.N - 1) * P1.ldw, P1.K, lane);
-  if (P1.lng) {
-    rv_load(g1, P1.lng, P1.K, lane);
-    rv_load(bb1, P1.lnb, P1.K, lane);
-  }
-  real_mask(rm1, P1.K, lane);
-  const float bia1 = gld(P1.b + min(o0 + (lane & 3), P1.N - 1));
-  // layer 2's k-slice: thread t owns outputs t and t + 256, their 16 weights of the slice (W2 rows
-  // are 16-B aligned: k0 is a multiple of 16) and the slice's LN1 affine (the same for every thread)
-  float4 w2s[2][4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int o = min((int)threadIdx.x + 256 * h, P2.N - 1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w2s[h][q] = gld4(P2.W + (size_t)o * P2.ldw + k0 + 4 * q);
-  }
-  float gs[16], bs[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 gg = P2.lng ? gld4(P2.lng + k0 + 4 * q) : make_float4(1.f, 1.f, 1.f, 1.f);
-    const float4 bv = P2.lng ? gld4(P2.lnb + k0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-    gs[4 * q] = gg.x; gs[4 * q + 1] = gg.y; gs[4 * q + 2] = gg.z; gs[4 * q + 3] = gg.w;
-    bs[4 * q] = bv.x; bs[4 * q + 1] = bv.y; bs[4 * q + 2] = bv.z; bs[4 * q + 3] = bv.w;
-  }
-  // 1. H0 of every query row (as act_kernel)
-#pragma unroll
-  for (int i = 0; i < NPASS; ++i) {
-    const int o = rsub + RPP * i;
-    const float4 w = w0r[i];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float z = w.x * xr[r][0];
-      z = z + w.y * xr[r][1];
-      z = z + w.z * xr[r][2];
-      z = z + w.w * xr[r][3];
-#pragma unroll
-      for (int m = TPR / 2; m >= 1; m >>= 1) z = z + __shfl_xor(z, m);
-      if (kg == 0) h0[r][o] = o < a.g.N0 ? fmaxf(z + b0r[i], 0.f) : 0.f;
-    }
-  }
-  __syncthreads();
-  TL_MARK(5);
-  // 2. layer 1 (4 columns per wave) into LDS
-  {
-    float x[R][8];
-#pragma unroll
-    for (int r = 0; r < R; ++r) rv_load_lds(x[r], h0[r], P1.K, lane);
-    if (P1.lng) {
-      float mean[R], rstd[R];
-      ln_fwd_rows_pk<R>(x, g1, bb1, rm1, 1.0f / (float)P1.K, mean, rstd);
-    }
-    float z[4][R];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-      for (int r = 0; r < R; ++r) z[jj][r] = wsum(rv_pdot(x[r], w1[jj], P1.K, lane));
-    const int j = lane & 3, rr = lane >> 2;
-    if (rr < R) {
-      float v = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-          if (jj == j && r == rr) v = z[jj][r];
-      s_h1[rr][wave * 4 + j] = (o0 + j < P1.N) ? fmaxf(v + bia1, 0.f) : 0.f;
-    }
-  }
-  __syncthreads();
-  TL_MARK(6);
-  // 3. the slice's partials: A, C, D per output, LN1 statistics per row (count nk, mean, M2)
-  float* my = part + (size_t)blockIdx.x * a.part_ld;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int o = threadIdx.x + 256 * h;
-    if (o < N2p) {
-      float wv[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        wv[4 * q] = w2s[h][q].x; wv[4 * q + 1] = w2s[h][q].y; wv[4 * q + 2] = w2s[h][q].z; wv[4 * q + 3] = w2s[h][q].w;
-      }
-      const bool live = o < P2.N;
-      float cc = 0.f, dd = 0.f, aa[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) aa[r] = 0.f;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        if (c >= nk) break;
-        const float wg = wv[c] * gs[c];
-        cc = cc + wg;
-        dd = dd + wv[c] * bs[c];
-#pragma unroll
-        for (int r = 0; r < R; ++r) aa[r] = aa[r] + wg * s_h1[r][c];
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) ast(my + r * N2p + o, live ? aa[r] : 0.f);
-      ast(my + R * N2p + o, live ? cc : 0.f);
-      ast(my + (R + 1) * N2p + o, live ? dd : 0.f);
-    }
-  }
-  if (threadIdx.x < R) {
-    const int r = threadIdx.x;
-    float m = 0.f;
-    for (int c = 0; c < nk; ++c) m = m + s_h1[r][c];
-    m = m / (float)nk;
-    float q = 0.f;
-    for (int c = 0; c < nk; ++c) {
-      const float d = s_h1[r][c] - m;
-      q = q + d * d;
-    }
-    ast(my + (R + 2) * N2p + 2 * r, m);
-    ast(my + (R + 2) * N2p + 2 * r + 1, q);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  TL_MARK(1);
-  if (threadIdx.x == 0)
-    s_flag = __hip_atomic_fetch_add((GAS int*)c1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
-  __syncthreads();
-  TL_MARK(2);
-  if (!s_flag) return;
-  // 4. the last arriver: the head's operands (in flight during the reduction), the partials summed
-  //    in workgroup order, LN1 statistics merged, z2, ReLU into LDS
-  const HeadProb& H = a.head[k];
-  constexpr int kPre = 8;
-  float w4[kPre][8], hg[8], hb[8];
-  if (wave < B) {
-#pragma unroll
-    for (int o = 0; o < kPre; ++o) rv_load(w4[o], H.W4 + (size_t)min(o, H.nout - 1) * H.ldw, H.ldw, lane);
-    if (H.lng) {
-      rv_load(hg, H.lng, H.ldh, lane);
-      rv_load(hb, H.lnb, H.ldh, lane);
-    }
-  }
-  const float b4 = lane < H.nout ? gld(H.b4 + lane) : 0.f;
-  if (threadIdx.x < R) {          // Chan's merge of the slices' (count, mean, M2), slice order
-    const int r = threadIdx.x;
-    float n = 0.f, mean = 0.f, m2 = 0.f;
-    for (int b = 0; b < nb; ++b) {
-      const float* st = part + (size_t)b * a.part_ld + (R + 2) * N2p + 2 * r;
-      const float nbk = (float)min(16, P1.N - 16 * b);
-      const float mb = ald(st), qb = ald(st + 1);
-      const float nn = n + nbk, d = mb - mean;
-      mean = mean + d * (nbk / nn);
-      m2 = m2 + qb + d * d * (n * nbk / nn);
-      n = nn;
-    }
-    s_st[r][0] = mean;
-    s_st[r][1] = P2.lng ? __builtin_amdgcn_rsqf(m2 / n + 1e-5f) : 1.f;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int o = threadIdx.x + 256 * h;
-    if (o < N2p) {
-      float aa[R], cc = 0.f, dd = 0.f;
-#pragma unroll
-      for (int r = 0; r < R; ++r) aa[r] = 0.f;
-      for (int b = 0; b < nb; ++b) {
-        const float* pb = part + (size_t)b * a.part_ld;
-#pragma unroll
-        for (int r = 0; r < R; ++r) aa[r] = aa[r] + ald(pb + r * N2p + o);
-        cc = cc + ald(pb + R * N2p + o);
-        dd = dd + ald(pb + (R + 1) * N2p + o);
-      }
-      const float b2 = o < P2.N ? gld(P2.b + o) : 0.f;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float z = P2.lng ? s_st[r][1] * (aa[r] - s_st[r][0] * cc) + dd + b2 : aa[r] + dd + b2;
-        s_h2[r][o] = o < P2.N ? fmaxf(z, 0.f) : 0.f;
-      }
-    }
-  }
-  __syncthreads();
-  TL_MARK(7);
-  // 5. LN2 + head of row `wave`, outputs to mapped host memory, completion flag
-  if (wave < B) {
-    float x[1][8], mean[1], rstd[1];
-    rv_load_lds(x[0], s_h2[wave], H.K3, lane);
-    if (H.lng) ln_fwd_rows<1>(x, hg, hb, H.K3, lane, mean, rstd);
-    float zl = 0.f;
-#pragma unroll
-    for (int o = 0; o < kPre; ++o) {
-      if (o >= H.nout) break;
-      const float z = wsum(rv_pdot(x[0], w4[o], H.K3, lane)) + __shfl(b4, o);
-      if (lane == o) zl = z;
-    }
-    for (int o = kPre; o < H.nout; ++o) {
-      float w[8];
-      rv_load(w, H.W4 + (size_t)o * H.ldw, H.ldw, lane);
-      const float z = wsum(rv_pdot(x[0], w, H.K3, lane)) + __shfl(b4, o);
-      if (lane == o) zl = z;
-    }
-    if (lane < H.nout) {
-      if (H.mode == kHeadPolicy) gst(H.out + ((size_t)wave * H.ldo + H.out_col + lane), a.max_action * tanhf(zl));
-      else gst(H.out + ((size_t)wave * H.ldo + lane), zl);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_store((GAS int*)c1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.flag) {
-      __threadfence_system();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.flag + k, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  TL_MARK(3);
-}
-
 // templated on NORM and with the problems in the kernel arguments: a runtime `norm` select on
 // the statistics loads compiled to a branch and a load drain per row (5 dependent load rounds)
 #ifndef TD3_LNBWD_RB
@@ -2883,6 +2653,11 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
       gst4(a.adam.V + ix, make_float4(vv[0], vv[1], vv[2], vv[3]));
       gst4(a.adam.P + ix, make_float4(pp[0], pp[1], pp[2], pp[3]));
       if (pol) gst4(a.adam.T + ix, make_float4(tt[0], tt[1], tt[2], tt[3]));
+      if (a.adam.P4) {        // the k-quad images: this thread's 4 elements are one 16-B piece
+        const int64_t iq = P.offW + ((int64_t)((k0 + tq) >> 2) * P.Np + n0 + tn) * 4;
+        gst4(a.adam.P4 + iq, make_float4(pp[0], pp[1], pp[2], pp[3]));
+        if (pol) gst4(a.adam.T4 + iq, make_float4(tt[0], tt[1], tt[2], tt[3]));
+      }
     }
     TL_MARK(3);
     return;
@@ -3933,22 +3708,7 @@ int launch_act(const ActArgs& a, int nprob, hipStream_t s) {
     set_error("launch_act: layer-0 rows of %d floats (K0 %d)", a.g.ldw0, a.g.K0);
     return -1;
   }
-  if (a.part) {                 // one hand-off (act2_kernel)
-    if (a.part_n2 < a.l2[0].N || (nprob > 1 && a.part_n2 < a.l2[1].N) || a.part_n2 > 512 ||
-        a.part_ld < (B <= 1 ? 3 : B <= 2 ? 4 : 6) * a.part_n2 + 8) {
-      set_error("launch_act: partial slab too small");
-      return -1;
-    }
-    if (a.g.K0 <= 32) {
-      if (B == 1) hipLaunchKernelGGL((act2_kernel<1, 8>), grid, dim3(256), 0, s, a);
-      else if (B == 2) hipLaunchKernelGGL((act2_kernel<2, 8>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((act2_kernel<4, 8>), grid, dim3(256), 0, s, a);
-    } else {
-      if (B == 1) hipLaunchKernelGGL((act2_kernel<1, 16>), grid, dim3(256), 0, s, a);
-      else if (B == 2) hipLaunchKernelGGL((act2_kernel<2, 16>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((act2_kernel<4, 16>), grid, dim3(256), 0, s, a);
-    }
-  } else if (a.g.K0 <= 32) {
+  if (a.g.K0 <= 32) {
     if (B == 1) hipLaunchKernelGGL((act_kernel<1, 8>), grid, dim3(256), 0, s, a);
     else if (B == 2) hipLaunchKernelGGL((act_kernel<2, 8>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((act_kernel<4, 8>), grid, dim3(256), 0, s, a);
@@ -4068,6 +3828,40 @@ int launch_local_sum(const LocalSumArgs& a, hipStream_t s) {
   }
   const int blocks = (int)std::min<int64_t>((a.size + 255) / 256, 2048);
   if (blocks > 0) hipLaunchKernelGGL(local_sum_kernel, dim3(blocks), dim3(256), 0, s, a);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
+// One thread per 16-B piece (n, k-quad j) of a matrix: a coalesced float4 read along k, a float4
+// store into the image (consecutive threads: consecutive j of one row; the stores scatter by Np * 16 B)
+__global__ __launch_bounds__(256) void w4_pack_kernel(W4PackArgs a) {
+  const int64_t total = a.first[a.nmat];
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < (int64_t)a.npair * total; e += (int64_t)gridDim.x * 256) {
+    const int pr = (int)(e / total);
+    const int64_t q = e - (int64_t)pr * total;
+    int m = 0;
+    while (m + 1 < a.nmat && q >= a.first[m + 1]) ++m;
+    const int64_t pc = q - a.first[m];
+    const int kq = a.Kp[m] >> 2;
+    const int n = (int)(pc / kq), j = (int)(pc - (int64_t)n * kq);
+    const float4 v = gld4(a.src[pr] + a.off[m] + (int64_t)n * a.Kp[m] + 4 * j);
+    gst4(a.dst[pr] + a.off[m] + ((int64_t)j * a.Np[m] + n) * 4, v);
+  }
+}
+
+int launch_w4_pack(const W4PackArgs& a, hipStream_t s) {
+  if (a.nmat < 1 || a.nmat > kMaxW4Mats || a.npair < 1 || a.npair > 2) {
+    set_error("launch_w4_pack: %d matrices, %d arena pairs", a.nmat, a.npair);
+    return -1;
+  }
+  for (int m = 0; m < a.nmat; ++m)
+    if (a.Kp[m] % 4 || a.first[m + 1] - a.first[m] != (int64_t)a.Np[m] * (a.Kp[m] / 4)) {
+      set_error("launch_w4_pack: matrix %d ranges", m);
+      return -1;
+    }
+  const int64_t n = (int64_t)a.npair * a.first[a.nmat];
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(w4_pack_kernel, dim3(blocks), dim3(256), 0, s, a);
   TD3_HIP(hipGetLastError());
   return 0;
 }

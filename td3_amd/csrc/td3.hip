@@ -68,6 +68,13 @@ struct Group {
   int64_t cap = 0;           // allocated floats per copy (>= size + 256: the sharded optimizer's
                              // rank slices of 4-float multiples may run past `size` into zero pads)
   float *P = nullptr, *T = nullptr, *M = nullptr, *V = nullptr, *G = nullptr;
+  // k-quad images of P and T (kernels.h GemmProb::wsk: W[n][4j .. 4j+3] at ((j * Np + n) * 4) inside a
+  // matrix's [offW, offW + Np * Kp) range), read by the forward GEMM stages of a plan with Plan::w4.
+  // Such a plan's dW stages (dw_kernel) write every updated weight to them as well; anything else
+  // that writes P / T (td3_set_params, another plan's optimizer) clears w4_valid and the next w4
+  // step repacks them first (ensure_w4).
+  float *P4 = nullptr, *T4 = nullptr;
+  bool w4_valid = false;
   std::vector<NetL> nets;
   std::vector<TensorRef> tensors;
   WnArgs wn{};               // weight normalization: the group's Linears (wn.nlin = 0 otherwise)
@@ -246,6 +253,7 @@ struct Plan {
   // rows' records, a loss once they are KBs (Humanoid: gather 4.8 + F_fwd0 23 us separate vs
   // 34 us fused)
   bool fuse_gather = false;
+  bool w4 = false;                      // forward weights read from the k-quad images (Group::P4 / T4)
   hipGraphExec_t graph[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   // the same bodies with the replay-ring gather captured in front (Philox draw path)
   hipGraphExec_t graph_g[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -370,6 +378,7 @@ struct td3_handle {
   std::shared_ptr<LocalGroup> local;          // td3_comm_init_local (comm stays null)
   int nranks = 1, rank = 0;
   bool dp_sharded = false;                    // the plan's optimizer steps are sharded (add_dw_stage)
+  bool w4_build = false;                      // the plan being built reads / maintains the k-quad images
   int64_t opt_gathered_it = -1;               // total_it of the last td3_dp_gather_optimizer_state
   std::vector<Stage>* last_body = nullptr;
   Ring* last_ring = nullptr;                  // the ring of the last td3_profile_stages (stage 0: its gather)
@@ -643,6 +652,55 @@ static bool l0r16_config(const std::vector<FwdItem>& items, int Bp, int* nct, in
   return false;
 }
 
+// The k-quad image of an arena copy (nullptr: none, or the plan being built does not use them)
+static const float* w4_of(const td3_handle* h, const float* base) {
+  if (!h->w4_build) return nullptr;
+  for (const Group* g : {&h->actor, &h->critic}) {
+    if (base == g->P) return g->P4;
+    if (base == g->T) return g->T4;
+  }
+  return nullptr;
+}
+
+// Forward GEMM weight loads from k-quad images (GemmProb::wsk).  An MFMA fragment load puts 16 (or
+// 32) consecutive output columns n in the 16 lanes of an access group, each reading 16 B of its own
+// weight row: 16 rows' lines per group instruction from the row-major [n][k] arena, 256 contiguous
+// bytes from the [k/4][n][4] image.  Measured on C2 with the image addressing of the arena itself
+// (TD3_W4FAKE, timing only): 10.08 k -> 10.95 k steps/s; CB_bwd2+TF_fwd01 14.5 -> 11.9 us, odd
+// F_fwd01 15.5 -> 12.1, even F_fwd01 18.3 -> 15.9, AF_fwd01 9.7 -> 8.1.  The images are maintained by
+// dw_kernel (Bp < 512) only: plans with split-K / 64-tile dW (Bp >= 512), data parallelism, weight
+// normalization or particle encoders read the row-major arena.  TD3_W4=0 turns them off.
+static bool w4_eligible(const td3_handle* h, int Bp) {
+  static const bool on = env_int("TD3_W4", 1) != 0;
+  return on && Bp < 512 && !h->particles && h->cfg.norm != 2 && !h->comm && !h->local;
+}
+
+// Before a w4 plan runs: the images of both groups rebuilt from P / T if anything else wrote those
+static int ensure_w4(td3_handle* h, hipStream_t s) {
+  if (!h->plan || !h->plan->w4) return 0;
+  for (Group* g : {&h->actor, &h->critic}) {
+    if (g->w4_valid) continue;
+    W4PackArgs a{};
+    a.src[0] = g->P;
+    a.dst[0] = g->P4;
+    a.src[1] = g->T;
+    a.dst[1] = g->T4;
+    a.npair = 2;
+    for (const NetL& n : g->nets)
+      for (const LinearL& L : n.lin) {
+        TD3_ARG(a.nmat < kMaxW4Mats, "internal: too many matrices for the k-quad pack");
+        a.off[a.nmat] = L.offW;
+        a.Np[a.nmat] = L.Np;
+        a.Kp[a.nmat] = L.Kp;
+        a.first[a.nmat + 1] = a.first[a.nmat] + (int64_t)L.Np * (L.Kp / 4);
+        ++a.nmat;
+      }
+    TD3_RC(launch_w4_pack(a, s));
+    g->w4_valid = true;
+  }
+  return 0;
+}
+
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
                           const std::vector<FwdItem>& items, int Bp, int B, const char* tag,
                           Counters* bump, int bump_actor, const RingSide* ring = nullptr,
@@ -744,6 +802,15 @@ static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<
       p.Kp = L.Kp;
       p.W = it.P + L.offW;
       p.ldw = L.Kp;
+      if (const float* q = w4_of(h, it.P)) {     // the k-quad image of the same weights
+        p.W = q + L.offW;
+        p.ldw = 4;
+        p.wsk = 4 * L.Np;
+        if (l0) {
+          p.ex[8] = const_cast<float*>(q + it.net->lin[0].offW);
+          p.w0sk = 4 * it.net->lin[0].Np;
+        }
+      }
       p.bias = it.P + L.offb;
       p.Nout = L.Np;
       p.C = it.e->H[l];
@@ -1122,6 +1189,11 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.adam.eps = h->adam[which].eps;
   a.adam.tau = (float)h->cfg.tau;
   a.adam.grad_scale = 1.0f;
+  if (h->w4_build) {                       // dw_kernel keeps the k-quad images current
+    TD3_ARG(!tile64 && g.P4 && g.T4, "internal: k-quad images in a plan without dw_kernel");
+    a.adam.P4 = g.P4;
+    a.adam.T4 = g.T4;
+  }
   const bool dp = h->comm != nullptr || h->local != nullptr;
   const bool wn = g.wn.nlin > 0;            // weight normalization: dW -> (dg, dv) in wn_kernel
   a.mode = (dp || wn) ? kDwGrad : (polyak ? kDwAdamPolyak : kDwAdam);
@@ -1390,6 +1462,8 @@ static int build_step(td3_handle* h, int B) {
   const int Bp = pad32(B);
   P->B = B;
   P->Bp = Bp;
+  h->w4_build = w4_eligible(h, Bp);
+  P->w4 = h->w4_build;
   const bool norm = h->cfg.norm == 1;
   const int sd = h->sd, ad = h->ad;
   P->ld_sa = pad32(sd + ad);
@@ -2218,6 +2292,7 @@ static int run_body(td3_handle* h, int actor_phase, int inj, hipStream_t s, Ring
     set_error("a td3_comm_init_local replica steps through td3_train_step_local only");
     return -1;
   }
+  TD3_RC(ensure_w4(h, s));
   Plan* P = h->plan.get();
   const bool fused = ring && P->fuse_gather;     // featured: the sample runs inside F_fwd0
   std::vector<Stage>& st = fused ? P->body_ring[actor_phase][inj] : P->body[actor_phase][inj];
@@ -2278,7 +2353,12 @@ static int build_plan(td3_handle* h, int B) {
   // the profiled stage list lives in the plan being replaced
   h->last_body = nullptr;
   h->last_ring = nullptr;
-  return h->particles ? build_step_particles(h, B) : build_step(h, B);
+  // the images are not maintained by every plan: the first step of a new one repacks them
+  h->actor.w4_valid = h->critic.w4_valid = false;
+  h->w4_build = false;
+  const int rc = h->particles ? build_step_particles(h, B) : build_step(h, B);
+  h->w4_build = false;
+  return rc;
 }
 
 static int ensure_plan(td3_handle* h, int B) {
@@ -2508,20 +2588,6 @@ static int build_act(td3_handle* h, int Bp, ActPlan** out) {
     float* oq[2] = {A->q[0], A->q[1]};
     A->act1 = A->hio && mk(A->a1_act, A->g01_act, A->gv_act[2], {&an}, h->actor.P, ea, oa, A->ldo, kHeadPolicy, ctr) &&
               mk(A->a1_q, A->g01_q, A->gv_q[2], {&q1, &q2}, h->critic.P, eq, oq, 1, kHeadQ, ctr + 8);
-    if (A->act1 && env_int("TD3_ACT1", 1) == 2) {     // one-hand-off form: the partial slab
-      const int n2p = std::max(pad32(an.lin[2].N), pad32(q1.lin[2].N));
-      const int ld = 6 * n2p + 8;                       // up to kGemvRows = 4 rows
-      const int nb = std::max((an.lin[1].N + 15) / 16, (q1.lin[1].N + 15) / 16);
-      float* slab = nullptr;
-      TD3_HIP(hipMalloc(&slab, (size_t)2 * 2 * nb * ld * sizeof(float)));   // act and eval_q, 2 networks
-      A->tables.push_back(slab);
-      A->a1_act.part = slab;
-      A->a1_q.part = slab + (size_t)2 * nb * ld;
-      for (ActArgs* x : {&A->a1_act, &A->a1_q}) {
-        x->part_ld = ld;
-        x->part_n2 = n2p;
-      }
-    }
     if (A->act1) {       // completion flags in the mapped block (io_floats reserves 4 * 64 floats of slack)
       float* hf = nullptr;
       A->a1_act.flag = reinterpret_cast<unsigned*>(io.take(64, &hf));
@@ -2773,7 +2839,7 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
   }
   h->actor.cap = ((h->actor.size + 255) & ~(int64_t)255) + 256;
   h->critic.cap = ((h->critic.size + 255) & ~(int64_t)255) + 256;
-  const size_t total = 5 * (size_t)(h->actor.cap + h->critic.cap);
+  const size_t total = 7 * (size_t)(h->actor.cap + h->critic.cap);
   hipError_t e = hipMalloc(&h->arena, total * sizeof(float));
   if (e != hipSuccess) {
     set_error("td3_create: hipMalloc failed: %s", hipGetErrorString(e));
@@ -2788,6 +2854,8 @@ int td3_create(const td3_config* cfg, td3_handle** out) {
     g->M = p; p += g->cap;
     g->V = p; p += g->cap;
     g->G = p; p += g->cap;
+    g->P4 = p; p += g->cap;
+    g->T4 = p; p += g->cap;
   }
   TD3_HIP(hipMalloc(&h->d_ctr, sizeof(Counters)));
   {
@@ -2991,6 +3059,7 @@ int td3_set_params(td3_handle* h, int which, const float* in, int64_t n) {
     }
   }
   TD3_HIP(hipMemcpy(base, host.data(), g->size * 4, hipMemcpyHostToDevice));
+  if (base == g->P || base == g->T) g->w4_valid = false;   // repacked by the next w4 step
   if (g->wn.nlin > 0 && (base == g->P || base == g->T)) {   // W = v * (g / ||v||) of the new (g, v)
     WnArgs w = g->wn;
     w.mode = kWnDerive;
@@ -3587,6 +3656,7 @@ int td3_profile_stages(td3_handle* h, rb_handle* rbh, int batch, int actor_phase
   std::vector<hipEvent_t> ev(n + 1);
   for (auto& e : ev) TD3_HIP(hipEventCreate(&e));
   hipStream_t s = h->stream;
+  TD3_RC(ensure_w4(h, s));
   TD3_RC(ring_begin_read(r, s));
   TD3_HIP(hipEventRecord(ev[0], s));
   if (!fused) TD3_RC(input_from_ring(h, r, P, false, s));

@@ -435,18 +435,17 @@ def test_large_batch_teacher_forced(B):
         _params_close(pol.critic_target.numpy_dict(), L.critic_target, L.lr, (step, "critic_target"))
 
 
-@pytest.mark.parametrize("variant", ["1", "2"])
 @pytest.mark.parametrize("n", [1, 2, 3, 4])
-def test_one_launch_query_equals_launch_chain(n, variant, monkeypatch):
+def test_one_launch_query_equals_launch_chain(n, monkeypatch):
     """select_action / eval_q of n <= 4 rows as ONE act_kernel launch (in-launch H1 hand-off, head in
-    the last-arriving workgroup; variant "2": act2_kernel, one hand-off of layer-2 partial sums)
-    against the gemv01 -> gemv -> head chain (TD3_ACT1=0) and the oracle.  Layer 0's dot products are summed in another order (4-column partials, butterfly):
+    the last-arriving workgroup) against the gemv01 -> gemv -> head chain (TD3_ACT1=0) and the
+    oracle.  Layer 0's dot products are summed in another order (4-column partials, butterfly):
     fp32 rounding apart, the same values (SURVEY §8c forward tolerance)."""
     from td3_amd import _lib
     S = featured_setup("hc_layer")
     outs = []
     st = np.random.RandomState(40 + n).standard_normal((n, S["sd"])).astype(np.float32)
-    for flag in (variant, "0"):
+    for flag in ("1", "0"):
         monkeypatch.setenv("TD3_ACT1", flag)
         pol, _ = _make(S)
         a = pol.select_action_batch(st)
