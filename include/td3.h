@@ -262,6 +262,10 @@ double td3_stage_flops(td3_handle* h, int i);
  * The tests take the ReLU masks of the step from it: where a pre-activation lies within fp32 rounding of
  * zero the oracle and the GPU may both be right about opposite masks (tests/test_gpu_gradients.py). */
 int td3_debug_activation(td3_handle* h, int eval, int layer, float* out, int rows, int cols);
+/* Test instrumentation: properties of the current step plan (0 before the first step): bit 0 = the forward
+ * GEMM stages read the k-quad weight images (td3.hip Group::P4 / T4; TD3_W4, Bp < 512 without data
+ * parallelism or weight normalization), bit 1 = the plan's optimizer steps are sharded over ranks. */
+int td3_debug_plan_flags(const td3_handle* h, int* flags);
 
 const char* td3_last_error(void);
 

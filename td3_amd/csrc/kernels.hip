@@ -2350,9 +2350,11 @@ __device__ __forceinline__ void adam_state_load(const DwArgs& a, const int64_t (
   }
 }
 
+// qidx (nullable): the elements' k-quad image indices (AdamArgs::P4 / T4), for weight matrices
 template <int N>
 __device__ __forceinline__ void apply_grads_loaded(const DwArgs& a, const AdamK& k, const int64_t (&idx)[N],
-                                                   const float (&g)[N], const bool (&ok)[N], AdamState<N>& st) {
+                                                   const float (&g)[N], const bool (&ok)[N], AdamState<N>& st,
+                                                   const int64_t* qidx = nullptr) {
   if (a.mode == kDwGrad) {
 #pragma unroll
     for (int e = 0; e < N; ++e)
@@ -2380,15 +2382,19 @@ __device__ __forceinline__ void apply_grads_loaded(const DwArgs& a, const AdamK&
     gst(a.adam.V + idx[e], vv[e]);
     gst(a.adam.P + idx[e], pp[e]);
     if (pol) gst(a.adam.T + idx[e], tt[e]);
+    if (qidx && a.adam.P4) {
+      gst(a.adam.P4 + qidx[e], pp[e]);
+      if (pol) gst(a.adam.T4 + qidx[e], tt[e]);
+    }
   }
 }
 
 template <int N>
 __device__ __forceinline__ void apply_grads(const DwArgs& a, const AdamK& k, const int64_t (&idx)[N],
-                                            const float (&g)[N], const bool (&ok)[N]) {
+                                            const float (&g)[N], const bool (&ok)[N], const int64_t* qidx = nullptr) {
   AdamState<N> st;
   adam_state_load<N>(a, idx, ok, st);
-  apply_grads_loaded<N>(a, k, idx, g, ok, st);
+  apply_grads_loaded<N>(a, k, idx, g, ok, st, qidx);
 }
 
 // The dZ rows' scale (unit-gradient rows: g_r; otherwise 1.0 from ldrs = 0) is requested with the
@@ -2789,7 +2795,7 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
   // Humanoid C_dw 49 -> 60 us)
   if (rh == 0) {
     const int kk = k0 + qk * 32 + i;
-    int64_t idx[16];
+    int64_t idx[16], qidx[16];
     float gq[16];
     bool ok[16];
 #pragma unroll
@@ -2798,9 +2804,10 @@ __global__ __launch_bounds__(512) void dw64_kernel(DwArgs a, int nb) {
       gq[r] = acc[r] + red[mfma_row(r, lane) * 33 + i];
       ok[r] = n < P.Np && kk < P.kvalid;           // kvalid <= Kp: columns past it keep their 0
       idx[r] = P.offW + (int64_t)n * P.Kp + kk;
+      qidx[r] = P.offW + ((int64_t)(kk >> 2) * P.Np + n) * 4 + (kk & 3);
     }
     TL_MARK(2);
-    apply_grads<16>(a, make_adam(a.adam, pw), idx, gq, ok);
+    apply_grads<16>(a, make_adam(a.adam, pw), idx, gq, ok, qidx);
     TL_MARK(3);
   }
 }
@@ -2926,7 +2933,7 @@ __global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
   __syncthreads();
   if (rh == 0) {
     const int kk = k0 + qk * 32 + i;
-    int64_t idx[16];
+    int64_t idx[16], qidx[16];
     float gq[16];
     bool ok[16];
 #pragma unroll
@@ -2935,9 +2942,10 @@ __global__ __launch_bounds__(512, 4) void dw64g_kernel(DwArgs a, int nb) {
       gq[r] = acc[r] + red[mfma_row(r, lane) * 33 + i];
       ok[r] = n < P.Np && kk < P.kvalid;           // kvalid <= Kp: columns past it keep their 0
       idx[r] = P.offW + (int64_t)n * P.Kp + kk;
+      qidx[r] = P.offW + ((int64_t)(kk >> 2) * P.Np + n) * 4 + (kk & 3);
     }
     TL_MARK(2);
-    apply_grads<16>(a, make_adam(a.adam, pw), idx, gq, ok);
+    apply_grads<16>(a, make_adam(a.adam, pw), idx, gq, ok, qidx);
     TL_MARK(3);
   }
 }
@@ -3286,6 +3294,11 @@ __global__ __launch_bounds__(256) void dwsk_combine_kernel(DwArgs a, DwSplit k) 
       gst4(a.adam.V + ix, make_float4(vv[0], vv[1], vv[2], vv[3]));
       gst4(a.adam.P + ix, make_float4(pp[0], pp[1], pp[2], pp[3]));
       if (pol) gst4(a.adam.T + ix, make_float4(tt[0], tt[1], tt[2], tt[3]));
+      if (a.adam.P4) {                                // the k-quad images (one 16-B piece)
+        const int64_t iq = P.offW + ((int64_t)(kk >> 2) * P.Np + n) * 4;
+        gst4(a.adam.P4 + iq, make_float4(pp[0], pp[1], pp[2], pp[3]));
+        if (pol) gst4(a.adam.T4 + iq, make_float4(tt[0], tt[1], tt[2], tt[3]));
+      }
     }
     return;
   }

@@ -668,11 +668,13 @@ static const float* w4_of(const td3_handle* h, const float* base) {
 // bytes from the [k/4][n][4] image.  Measured on C2 with the image addressing of the arena itself
 // (TD3_W4FAKE, timing only): 10.08 k -> 10.95 k steps/s; CB_bwd2+TF_fwd01 14.5 -> 11.9 us, odd
 // F_fwd01 15.5 -> 12.1, even F_fwd01 18.3 -> 15.9, AF_fwd01 9.7 -> 8.1.  The images are maintained by
-// dw_kernel (Bp < 512) only: plans with split-K / 64-tile dW (Bp >= 512), data parallelism, weight
-// normalization or particle encoders read the row-major arena.  TD3_W4=0 turns them off.
+// the dW kernels' optimizer epilogues (dw_kernel, dw64 / dw64g, the split-K combine); plans whose
+// optimizer runs elsewhere (data parallelism: flat Adam after the exchange; weight normalization:
+// wn_kernel) and the particle learner read the row-major arena.  TD3_W4=0 turns them off.
 static bool w4_eligible(const td3_handle* h, int Bp) {
-  static const bool on = env_int("TD3_W4", 1) != 0;
-  return on && Bp < 512 && !h->particles && h->cfg.norm != 2 && !h->comm && !h->local;
+  (void)Bp;
+  const bool on = env_int("TD3_W4", 1) != 0;     // read at every plan build (tests switch it)
+  return on && !h->particles && h->cfg.norm != 2 && !h->comm && !h->local;
 }
 
 // Before a w4 plan runs: the images of both groups rebuilt from P / T if anything else wrote those
@@ -1189,8 +1191,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
   a.adam.eps = h->adam[which].eps;
   a.adam.tau = (float)h->cfg.tau;
   a.adam.grad_scale = 1.0f;
-  if (h->w4_build) {                       // dw_kernel keeps the k-quad images current
-    TD3_ARG(!tile64 && g.P4 && g.T4, "internal: k-quad images in a plan without dw_kernel");
+  if (h->w4_build) {                       // the dW kernels keep the k-quad images current
+    TD3_ARG(g.P4 && g.T4, "internal: k-quad images not allocated");
     a.adam.P4 = g.P4;
     a.adam.T4 = g.T4;
   }
@@ -3734,6 +3736,12 @@ int td3_probe_kernel(td3_handle* h, rb_handle* rb, int batch, const char* kernel
   *launches = h->probe_used / 2;
   h->probe_used = 0;
   return rc;
+}
+
+int td3_debug_plan_flags(const td3_handle* h, int* flags) {
+  TD3_ARG(h && flags, "null argument");
+  *flags = h->plan ? ((h->plan->w4 ? 1 : 0) | (h->dp_sharded ? 2 : 0)) : 0;
+  return 0;
 }
 
 int td3_debug_activation(td3_handle* h, int eval, int layer, float* out, int rows, int cols) {
