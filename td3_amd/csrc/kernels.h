@@ -301,7 +301,15 @@ int launch_rows2(int kind1, int kind2, int n1, const GemmTable& t, int Bp, hipSt
 int launch_heads(const HeadArgs& a, int nprob, hipStream_t s);
 int launch_lnbwd_rows(const LnBwdTable& tab, int nprob, int Bp, int norm, hipStream_t s);
 int launch_dw(const DwArgs& a, int nblocks, hipStream_t s);
-int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s);
+// The flat optimizer's view of the images: the range it updates starts at arena offset `base`; a
+// float4 inside matrix m ([off, off + Np * Kp), off % 4 == 0) is also stored at its image piece
+struct W4Map {
+  float* P4; float* T4;         // image bases (arena offset 0); P4 null: no images
+  int64_t base;
+  int nmat;
+  int64_t off[8]; int Np[8], Kp[8];
+};
+int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s, const W4Map* w4 = nullptr);
 // Data-parallel replicas in one process (td3_comm_init_local): arena k <- sum over j of arena j,
 // summed in replica order (the same value lands in every replica, like a ring all-reduce).
 constexpr int kMaxLocalReplicas = 8;

@@ -3321,7 +3321,7 @@ __global__ __launch_bounds__(256) void dwsk_combine_kernel(DwArgs a, DwSplit k) 
 // The flat optimizer pass of the data-parallel path (after the all-reduce): 4 elements per thread
 // and array as one float4 (arenas and bucket ranges are multiples of 32 floats; launch_adam_flat
 // checks), every load of the 4 elements requested before the first store.
-__global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, int polyak) {
+__global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, int polyak, W4Map w) {
   const AdamK k = make_adam(a);
   const int64_t n4 = n >> 2;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
@@ -3340,6 +3340,18 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, int64_t n, i
     gst4(a.V + e, make_float4(vv[0], vv[1], vv[2], vv[3]));
     gst4(a.P + e, make_float4(pp[0], pp[1], pp[2], pp[3]));
     if (polyak) gst4(a.T + e, make_float4(tt[0], tt[1], tt[2], tt[3]));
+    if (w.P4) {                                      // the k-quad images of the weight matrices
+      const int64_t j = w.base + e;
+      for (int m = 0; m < w.nmat; ++m) {
+        const int64_t r = j - w.off[m];
+        if (r < 0 || r >= (int64_t)w.Np[m] * w.Kp[m]) continue;
+        const int nn = (int)(r / w.Kp[m]), kq = (int)(r - (int64_t)nn * w.Kp[m]) >> 2;
+        const int64_t iq = w.off[m] + ((int64_t)kq * w.Np[m] + nn) * 4;
+        gst4(w.P4 + iq, make_float4(pp[0], pp[1], pp[2], pp[3]));
+        if (polyak) gst4(w.T4 + iq, make_float4(tt[0], tt[1], tt[2], tt[3]));
+        break;
+      }
+    }
   }
 }
 
@@ -3807,14 +3819,24 @@ int launch_dw_split(const DwArgs& a, const DwSplit& k, hipStream_t s) {
   return 0;
 }
 
-int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s) {
+int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s, const W4Map* w4) {
   auto al16 = [](const float* p) { return ((uintptr_t)p & 15) == 0; };
   if ((n & 3) || !al16(a.P) || !al16(a.G) || !al16(a.M) || !al16(a.V) || (polyak && !al16(a.T))) {
     set_error("launch_adam_flat: the range must be float4-aligned (n %% 4 == 0, 16-B aligned arenas)");
     return -1;
   }
+  W4Map w{};
+  if (w4 && w4->P4) {
+    w = *w4;
+    bool ok = w.nmat >= 1 && w.nmat <= 8 && (w.base & 3) == 0 && (!polyak || w.T4);
+    for (int m = 0; ok && m < w.nmat; ++m) ok = (w.off[m] & 3) == 0 && w.Kp[m] % 4 == 0;
+    if (!ok) {
+      set_error("launch_adam_flat: bad k-quad image map");
+      return -1;
+    }
+  }
   const int blocks = (int)std::min<int64_t>((n / 4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, a, n, polyak);
+  hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, a, n, polyak, w);
   TD3_HIP(hipGetLastError());
   return 0;
 }

@@ -668,13 +668,37 @@ static const float* w4_of(const td3_handle* h, const float* base) {
 // bytes from the [k/4][n][4] image.  Measured on C2 with the image addressing of the arena itself
 // (TD3_W4FAKE, timing only): 10.08 k -> 10.95 k steps/s; CB_bwd2+TF_fwd01 14.5 -> 11.9 us, odd
 // F_fwd01 15.5 -> 12.1, even F_fwd01 18.3 -> 15.9, AF_fwd01 9.7 -> 8.1.  The images are maintained by
-// the dW kernels' optimizer epilogues (dw_kernel, dw64 / dw64g, the split-K combine); plans whose
-// optimizer runs elsewhere (data parallelism: flat Adam after the exchange; weight normalization:
-// wn_kernel) and the particle learner read the row-major arena.  TD3_W4=0 turns them off.
+// the dW kernels' optimizer epilogues (dw_kernel, dw64 / dw64g, the split-K combine) and, in
+// data-parallel plans (flat Adam after the exchange), by a pack stage behind it (push_w4_pack).
+// Weight normalization (wn_kernel derives W) and the particle learner read the row-major arena.
+// TD3_W4=0 turns them off.
 static bool w4_eligible(const td3_handle* h, int Bp) {
   (void)Bp;
   const bool on = env_int("TD3_W4", 1) != 0;     // read at every plan build (tests switch it)
-  return on && !h->particles && h->cfg.norm != 2 && !h->comm && !h->local;
+  return on && !h->particles && h->cfg.norm != 2;
+}
+
+// The pack of a group's forward weights (layers 0-2: the heads are read by the row kernels) from P
+// (and T) into their images
+static int w4_pack_args(const Group& g, bool with_t, W4PackArgs* out) {
+  W4PackArgs a{};
+  a.src[0] = g.P;
+  a.dst[0] = g.P4;
+  a.src[1] = g.T;
+  a.dst[1] = g.T4;
+  a.npair = with_t ? 2 : 1;
+  for (const NetL& n : g.nets)
+    for (int l = 0; l < 3; ++l) {
+      const LinearL& L = n.lin[l];
+      TD3_ARG(a.nmat < kMaxW4Mats, "internal: too many matrices for the k-quad pack");
+      a.off[a.nmat] = L.offW;
+      a.Np[a.nmat] = L.Np;
+      a.Kp[a.nmat] = L.Kp;
+      a.first[a.nmat + 1] = a.first[a.nmat] + (int64_t)L.Np * (L.Kp / 4);
+      ++a.nmat;
+    }
+  *out = a;
+  return 0;
 }
 
 // Before a w4 plan runs: the images of both groups rebuilt from P / T if anything else wrote those
@@ -682,25 +706,41 @@ static int ensure_w4(td3_handle* h, hipStream_t s) {
   if (!h->plan || !h->plan->w4) return 0;
   for (Group* g : {&h->actor, &h->critic}) {
     if (g->w4_valid) continue;
-    W4PackArgs a{};
-    a.src[0] = g->P;
-    a.dst[0] = g->P4;
-    a.src[1] = g->T;
-    a.dst[1] = g->T4;
-    a.npair = 2;
-    for (const NetL& n : g->nets)
-      for (const LinearL& L : n.lin) {
-        TD3_ARG(a.nmat < kMaxW4Mats, "internal: too many matrices for the k-quad pack");
-        a.off[a.nmat] = L.offW;
-        a.Np[a.nmat] = L.Np;
-        a.Kp[a.nmat] = L.Kp;
-        a.first[a.nmat + 1] = a.first[a.nmat] + (int64_t)L.Np * (L.Kp / 4);
-        ++a.nmat;
-      }
+    W4PackArgs a;
+    TD3_RC(w4_pack_args(*g, true, &a));
     TD3_RC(launch_w4_pack(a, s));
     g->w4_valid = true;
   }
   return 0;
+}
+
+// The flat optimizer's image map of a group's forward weights (P4 null when the plan being built does
+// not use the images); `base`: the arena offset of the range it updates
+static W4Map w4_map(const td3_handle* h, const Group& g, int64_t base) {
+  W4Map w{};
+  if (!h->w4_build) return w;
+  w.P4 = g.P4;
+  w.T4 = g.T4;
+  w.base = base;
+  for (const NetL& n : g.nets)
+    for (int l = 0; l < 3 && w.nmat < 8; ++l) {
+      w.off[w.nmat] = n.lin[l].offW;
+      w.Np[w.nmat] = n.lin[l].Np;
+      w.Kp[w.nmat] = n.lin[l].Kp;
+      ++w.nmat;
+    }
+  return w;
+}
+
+// The sharded data-parallel step updates 1/N of P per rank and all-gathers P: the images are
+// repacked by a stage of their own behind it (the dW kernels run gradient-only in data-parallel
+// plans; the replicated flat optimizer of the all-reduce schedules writes the images itself)
+static void push_w4_pack(td3_handle* h, std::vector<Stage>& st, const Group& g, bool polyak, const char* tag) {
+  if (!h->w4_build) return;
+  W4PackArgs a;
+  if (w4_pack_args(g, polyak, &a)) return;
+  st.push_back({std::string(tag) + "_w4", [=](hipStream_t s) { return launch_w4_pack(a, s); }, 0,
+                "td3::w4_pack_kernel"});
 }
 
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
@@ -1254,6 +1294,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       const int64_t nb = end - off;
       AdamArgs ar = a.adam;
       ar.P += off; ar.G += off; ar.M += off; ar.V += off; ar.T += off;
+      const W4Map wm = w4_map(h, g, off);
       ar.grad_scale = 1.0f / (float)h->nranks;
       float* Gb = g.G + off;
       Stage x{std::string(tag) + "_" + std::to_string(b) + "_allreduce",
@@ -1270,7 +1311,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
                   set_error("ncclAllReduce: %s", ncclGetErrorString(r));
                   return -2;
                 }
-                TD3_RC(launch_adam_flat(ar, nb, pol, cs));
+                TD3_RC(launch_adam_flat(ar, nb, pol, cs, &wm));
                 if (!first) TD3_HIP(hipEventRecord(done, cs));
                 return 0;
               },
@@ -1278,7 +1319,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       x.collective = which == 1 ? 0 : 1;
       x.coll_off = off;
       x.coll_n = nb;
-      x.after = [=](hipStream_t s) { return launch_adam_flat(ar, nb, pol, s); };
+      x.after = [=](hipStream_t s) { return launch_adam_flat(ar, nb, pol, s, &wm); };
       exch.push_back(x);
     }
     for (auto& x : exch) st.push_back(x);          // dW_0, dW_1, exchange 0 (comm), exchange 1 (step)
@@ -1374,6 +1415,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       st.push_back({std::string(tag) + "_polyak", [=](hipStream_t s) { return launch_polyak_flat(Tp, Pp, n, tau, s); },
                     0, "td3::polyak_flat_kernel"});
     }
+    push_w4_pack(h, st, g, polyak, tag);
     return 0;
   }
   if (dp) {
@@ -1405,8 +1447,9 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     st.push_back({std::string(tag) + "_wn", [=](hipStream_t s) { return launch_wn(w, s); }, 0, "td3::wn_kernel"});
   } else if (dp) {
     const int64_t n = g.size;
+    const W4Map wm = w4_map(h, g, 0);
     st.push_back({std::string(tag) + "_adam",
-                  [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s); }, 0,
+                  [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s, &wm); }, 0,
                   "td3::adam_flat_kernel"});
   }
   return 0;
@@ -3557,6 +3600,7 @@ int td3_train_step_local(td3_handle** hs, rb_handle** rbs, int n, int batch, con
     TD3_ARG(r->device == h->cfg.device, "replay buffer lives on another device");
     if (h->stream != s) TD3_HIP(hipStreamSynchronize(h->stream));
     TD3_RC(ensure_plan(h, batch));
+    TD3_RC(ensure_w4(h, s));
     TD3_RC(bind_ring(h, r));
     TD3_RC(ring_begin_read(r, s));
   }

@@ -76,3 +76,44 @@ def test_k_quad_images_bit_identical(name, monkeypatch):
         for g, (u, v) in enumerate(zip(x, y)):
             assert np.array_equal(u, v), (name, phase, ("actor", "critic", "actor_target", "critic_target")[g],
                                           int(np.sum(u != v)))
+
+
+@pytest.mark.parametrize("name,b,shard,buckets", [("hc_layer", 128, "1", "0"), ("hc_layer", 128, "0", "0"),
+                                                  ("hum_layer", 1024, "1", "1")])
+def test_k_quad_images_data_parallel(name, b, shard, buckets, monkeypatch):
+    """Data-parallel plans (two td3_comm_init_local replicas) update P / T with the flat optimizer
+    behind the exchange and repack the images in a stage of their own (push_w4_pack): the sharded and
+    the all-reduce schedules, and Humanoid's overlapped two-bucket critic, bit-identical to the
+    row-major plans over free-running Philox steps and a mid-run set_weights."""
+    from td3_amd.data_parallel import local_group, train_local
+    S = featured_setup(name)
+    monkeypatch.setenv("TD3_DP_SHARD", shard)
+    monkeypatch.setenv("TD3_DP_BUCKETS", buckets)
+    res = []
+    for w4 in ("1", "0"):
+        monkeypatch.setenv("TD3_W4", w4)
+        pols, rbs = [], []
+        for _ in range(2):
+            p, rb = _make(S)
+            pols.append(p)
+            rbs.append(rb)
+        local_group(pols)
+        snaps = []
+        for _ in range(5):
+            train_local(pols, rbs, b)
+        assert _flags(pols[0]) & 1 == int(w4)
+        snaps.append([x for p in pols for x in _snap(p)])
+        rs = np.random.RandomState(9)
+        nd = lambda d: {k: (v + 0.01 * rs.standard_normal(v.shape)).astype(np.float32) for k, v in d.items()}
+        new = [nd(pols[0].actor.numpy_dict()), nd(pols[0].critic.numpy_dict())]
+        for p in pols:
+            p.set_weights(*new)
+        for _ in range(4):
+            train_local(pols, rbs, b)
+        snaps.append([x for p in pols for x in _snap(p)])
+        for p in pols:
+            p.sync()
+        res.append(snaps)
+    for phase, (x, y) in enumerate(zip(*res)):
+        for i, (u, v) in enumerate(zip(x, y)):
+            assert np.array_equal(u, v), (name, shard, phase, i, int(np.sum(u != v)))
