@@ -310,6 +310,7 @@ struct W4Map {
   int64_t off[8]; int Np[8], Kp[8];
 };
 int launch_adam_flat(const AdamArgs& a, int64_t n, int polyak, hipStream_t s, const W4Map* w4 = nullptr);
+int launch_polyak_w4(float* T, const float* P, int64_t n, float tau, const W4Map& w, hipStream_t s);
 // Data-parallel replicas in one process (td3_comm_init_local): arena k <- sum over j of arena j,
 // summed in replica order (the same value lands in every replica, like a ring all-reduce).
 constexpr int kMaxLocalReplicas = 8;

@@ -3901,6 +3901,41 @@ int launch_w4_pack(const W4PackArgs& a, hipStream_t s) {
   return 0;
 }
 
+// Polyak over a whole arena (the sharded data-parallel step, behind its all-gather) that also
+// refreshes the k-quad images of the weight matrices from the gathered P and the new T (w.base = 0)
+__global__ __launch_bounds__(256) void polyak_w4_kernel(float* T, const float* P, int64_t n, float tau, float omt,
+                                                        W4Map w) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < (n >> 2); i += (int64_t)gridDim.x * 256) {
+    const int64_t e = 4 * i;
+    const float4 p4 = gld4(P + e), t4 = gld4(T + e);
+    const float4 o = make_float4(tau * p4.x + omt * t4.x, tau * p4.y + omt * t4.y, tau * p4.z + omt * t4.z,
+                                 tau * p4.w + omt * t4.w);
+    gst4(T + e, o);
+    for (int m = 0; m < w.nmat; ++m) {
+      const int64_t r = e - w.off[m];
+      if (r < 0 || r >= (int64_t)w.Np[m] * w.Kp[m]) continue;
+      const int nn = (int)(r / w.Kp[m]), kq = (int)(r - (int64_t)nn * w.Kp[m]) >> 2;
+      const int64_t iq = w.off[m] + ((int64_t)kq * w.Np[m] + nn) * 4;
+      gst4(w.P4 + iq, p4);
+      gst4(w.T4 + iq, o);
+      break;
+    }
+  }
+}
+
+int launch_polyak_w4(float* T, const float* P, int64_t n, float tau, const W4Map& w, hipStream_t s) {
+  if ((n & 3) || ((uintptr_t)T & 15) || ((uintptr_t)P & 15) || !w.P4 || !w.T4 || w.base != 0 || w.nmat < 1 ||
+      w.nmat > 8) {
+    set_error("launch_polyak_w4: float4-aligned whole arena and an image map required");
+    return -1;
+  }
+  const int blocks = (int)std::min<int64_t>((n / 4 + 255) / 256, 2048);
+  const float omt = (float)(1.0 - (double)tau);
+  hipLaunchKernelGGL(polyak_w4_kernel, dim3(blocks), dim3(256), 0, s, T, P, n, tau, omt, w);
+  TD3_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_polyak_flat(float* T, const float* P, int64_t n, float tau, hipStream_t s) {
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
   const float omt = (float)(1.0 - (double)tau);

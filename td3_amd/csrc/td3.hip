@@ -1408,6 +1408,15 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     x.coll_slice = slice;
     x.after = [=](hipStream_t s) { return launch_adam_flat(as, slice, 0, s); };
     st.push_back(x);
+    if (polyak && h->w4_build) {        // Polyak and both images in one pass over the gathered arena
+      float* Tp = g.T;
+      const int64_t n = g.size;
+      const float tau = (float)h->cfg.tau;
+      const W4Map wm = w4_map(h, g, 0);
+      st.push_back({std::string(tag) + "_polyak", [=](hipStream_t s) { return launch_polyak_w4(Tp, Pp, n, tau, wm, s); },
+                    0, "td3::polyak_w4_kernel"});
+      return 0;
+    }
     if (polyak) {
       float* Tp = g.T;
       const int64_t n = g.size;
@@ -1415,7 +1424,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       st.push_back({std::string(tag) + "_polyak", [=](hipStream_t s) { return launch_polyak_flat(Tp, Pp, n, tau, s); },
                     0, "td3::polyak_flat_kernel"});
     }
-    push_w4_pack(h, st, g, polyak, tag);
+    push_w4_pack(h, st, g, false, tag);
     return 0;
   }
   if (dp) {

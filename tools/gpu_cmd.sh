@@ -1,10 +1,9 @@
 set -o pipefail
-F=gpurun_out/final
-mkdir -p $F
+mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-TD3_LIB=tools/exp/libtd3hip_tl.so timeout -k 10 200 python3 tools/tl_probe.py > $F/timeline_halfcheetah.txt 2>&1; echo "tl hc rc=$?"
-TL_SHAPE=376,17,1024 TD3_LIB=tools/exp/libtd3hip_tl.so timeout -k 10 200 python3 tools/tl_probe.py > $F/timeline_humanoid.txt 2>&1; echo "tl hum rc=$?"
-for c in halfcheetah pendulum humanoid; do
-  a=""; [ $c = humanoid ] && a="--steps 600 --warmup 50"
-  timeout -k 10 500 python3 bench.py --config $c $a > $F/bench2_$c.json 2> $F/bench2_$c.err; echo "bench $c rc=$? $(tail -c 300 $F/bench2_$c.json | cut -c1-200)"
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_w4.py tests/test_gpu_data_parallel.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pw4.log 2>&1; rc=$?; echo "w4+dp tests rc=$rc"; tail -3 gpurun_out/pw4.log
+[ $rc -ne 0 ] && exit $rc
+for v in 0 1 0 1; do
+TD3_DP_SHARD=2 TD3_W4=$v timeout -k 10 200 python3 bench.py --dp-self --steps 2000 --warmup 100 --no-cpu-baseline --no-roofline > gpurun_out/b_w4ds_$v.json 2>/dev/null; echo "dp-self shard w4=$v rc=$?"; python3 -c "
+import json;d=json.loads(open('gpurun_out/b_w4ds_$v.json').read().strip().splitlines()[-1]);print(d['value'],d.get('runs'))"
 done
