@@ -340,8 +340,10 @@ __device__ __forceinline__ void l0_load_x(const GemmProb& P, const RingSide& rs,
   const bool t0 = c.nt == 0;
   uint64_t step = 0, n = 0;
   if constexpr (GATHER) {
+#ifndef TD3_KO_REC
     step = (uint64_t)(rs.ctr->total_it + 1);
     n = (uint64_t)*rs.d_size;
+#endif
   }
   const int col = i;
   const bool valid = i < K0;
@@ -352,7 +354,11 @@ __device__ __forceinline__ void l0_load_x(const GemmProb& P, const RingSide& rs,
 #pragma unroll
     for (int rr = 0; rr < kL0R; ++rr) {
       const int grow = c.m0 + c.wave * kRPW + 2 * rr + h;
+#ifdef TD3_KO_REC    // knockout experiment (wrong samples): consecutive rows, no counter / size loads
+      X.idx[rr] = grow < P.B ? (int64_t)grow + (int64_t)(step + n) : -1;
+#else
       X.idx[rr] = grow < P.B ? (int64_t)philox_index(rs.seed, step, (uint32_t)grow, n) : -1;
+#endif
     }
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -1702,9 +1708,13 @@ __global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob,
   int64_t idx = 0;
   float xv, rw = 0.f;
   if constexpr (GATHER) {
+#ifdef TD3_KO_REC
+    idx = grow_x < P.B ? (int64_t)grow_x : -1;
+#else
     const uint64_t step = (uint64_t)(tab.rs.ctr->total_it + 1);
     const uint64_t n = (uint64_t)*tab.rs.d_size;
     idx = grow_x < P.B ? (int64_t)philox_index(tab.rs.seed, step, (uint32_t)grow_x, n) : -1;
+#endif
     __builtin_amdgcn_sched_barrier(0);
     const float* rec = tab.rs.data + (size_t)(idx >= 0 ? idx : 0) * tab.rs.rec;
     xv = gld(rec + P.exi[0] + (xcol < K0 ? xcol : 0));
@@ -2610,10 +2620,12 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
     const bool grad_only = a.mode == kDwGrad, pol = a.mode == kDwAdamPolyak;
     float4 sm4 = make_float4(0.f, 0.f, 0.f, 0.f), sv4 = sm4, sp4 = sm4, st4 = sm4;
     if (!grad_only) {
+#ifndef TD3_KO_ADAM   // knockout experiment (wrong optimizer): no moment / parameter loads
       sm4 = gld4(a.adam.M + ix);
       sv4 = gld4(a.adam.V + ix);
       sp4 = gld4(a.adam.P + ix);
       st4 = gld4((pol ? a.adam.T : a.adam.P) + ix);
+#endif
     }
     for (int rc = cb; rc < ce; rc += 2) {
       dw_scale<SC>(a0, c0);
@@ -2655,11 +2667,17 @@ __global__ __launch_bounds__(256, TD3_DW_OCC) void dw_kernel(DwArgs a, int nb) {
         pp[e] = pp[e] + (k.negss * mm[e]) / denom;
         tt[e] = k.tau * pp[e] + k.omt * tt[e];
       }
+#ifndef TD3_KO_ADAM
       gst4(a.adam.M + ix, make_float4(mm[0], mm[1], mm[2], mm[3]));
       gst4(a.adam.V + ix, make_float4(vv[0], vv[1], vv[2], vv[3]));
+#endif
       gst4(a.adam.P + ix, make_float4(pp[0], pp[1], pp[2], pp[3]));
       if (pol) gst4(a.adam.T + ix, make_float4(tt[0], tt[1], tt[2], tt[3]));
+#ifdef TD3_KO_IMGST
+      if (false) {
+#else
       if (a.adam.P4) {        // the k-quad images: this thread's 4 elements are one 16-B piece
+#endif
         const int64_t iq = P.offW + ((int64_t)((k0 + tq) >> 2) * P.Np + n0 + tn) * 4;
         gst4(a.adam.P4 + iq, make_float4(pp[0], pp[1], pp[2], pp[3]));
         if (pol) gst4(a.adam.T4 + iq, make_float4(tt[0], tt[1], tt[2], tt[3]));
