@@ -1661,6 +1661,9 @@ __global__ __launch_bounds__(64 * kNW, (W1 == 4 || W2 == 4) ? 4 : (W1 == kWn4x2 
 //  4. layer 1: wave (c = w % NCT, kq = w / NCT): 16 x 16 columns 16c.., K range kq of WK, chunks of
 //     32 (lane group g: k = kb + 8g + s, 2 ds_read_b128 per row chunk), partials summed through LDS.
 constexpr int kR16XS = 36;      // LDS row stride of the staged 16 input rows
+#ifndef TD3_L0R16_KS8
+#define TD3_L0R16_KS8 1
+#endif
 
 template <int NCT, int WK, bool GATHER>
 __global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob, int tb1, int tb2, int tb3, int Bp,
@@ -1811,12 +1814,23 @@ __global__ __launch_bounds__(64 * NCT * WK) void l0r16_kernel(int nb, int nprob,
     const int ks = min(K0, 8);                  // MFMA s reads k = 8g + s: all past K0 when s >= K0
     f32x4 acc0[kQ0];
 #pragma unroll
-    for (int q = 0; q < kQ0; ++q) {
-      acc0[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (wave + NW * q >= n0t) continue;
+    for (int q = 0; q < kQ0; ++q) acc0[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (TD3_L0R16_KS8 && ks == 8) {             // inputs of >= 8 features: no per-MFMA branches
 #pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2)
-        if (s2 < ks) acc0[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w0[q][s2], acc0[q], 0, 0, 0);
+      for (int q = 0; q < kQ0; ++q) {
+        if (wave + NW * q >= n0t) continue;
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+          acc0[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w0[q][s2], acc0[q], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kQ0; ++q) {
+        if (wave + NW * q >= n0t) continue;
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+          if (s2 < ks) acc0[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w0[q][s2], acc0[q], 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int q = 0; q < kQ0; ++q) {

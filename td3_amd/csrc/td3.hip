@@ -716,31 +716,35 @@ static int ensure_w4(td3_handle* h, hipStream_t s) {
 
 // The flat optimizer's image map of a group's forward weights (P4 null when the plan being built does
 // not use the images); `base`: the arena offset of the range it updates
-static W4Map w4_map(const td3_handle* h, const Group& g, int64_t base) {
+static int w4_map(const td3_handle* h, const Group& g, int64_t base, W4Map* out) {
   W4Map w{};
-  if (!h->w4_build) return w;
-  w.P4 = g.P4;
-  w.T4 = g.T4;
-  w.base = base;
-  for (const NetL& n : g.nets)
-    for (int l = 0; l < 3 && w.nmat < 8; ++l) {
-      w.off[w.nmat] = n.lin[l].offW;
-      w.Np[w.nmat] = n.lin[l].Np;
-      w.Kp[w.nmat] = n.lin[l].Kp;
-      ++w.nmat;
-    }
-  return w;
+  if (h->w4_build) {
+    w.P4 = g.P4;
+    w.T4 = g.T4;
+    w.base = base;
+    for (const NetL& n : g.nets)
+      for (int l = 0; l < 3; ++l) {
+        TD3_ARG(w.nmat < 8, "internal: too many matrices for the flat optimizer's image map");
+        w.off[w.nmat] = n.lin[l].offW;
+        w.Np[w.nmat] = n.lin[l].Np;
+        w.Kp[w.nmat] = n.lin[l].Kp;
+        ++w.nmat;
+      }
+  }
+  *out = w;
+  return 0;
 }
 
 // The sharded data-parallel step updates 1/N of P per rank and all-gathers P: the images are
 // repacked by a stage of their own behind it (the dW kernels run gradient-only in data-parallel
 // plans; the replicated flat optimizer of the all-reduce schedules writes the images itself)
-static void push_w4_pack(td3_handle* h, std::vector<Stage>& st, const Group& g, bool polyak, const char* tag) {
-  if (!h->w4_build) return;
+static int push_w4_pack(td3_handle* h, std::vector<Stage>& st, const Group& g, bool polyak, const char* tag) {
+  if (!h->w4_build) return 0;
   W4PackArgs a;
-  if (w4_pack_args(g, polyak, &a)) return;
+  TD3_RC(w4_pack_args(g, polyak, &a));
   st.push_back({std::string(tag) + "_w4", [=](hipStream_t s) { return launch_w4_pack(a, s); }, 0,
                 "td3::w4_pack_kernel"});
+  return 0;
 }
 
 static int add_fwd_stages(td3_handle* h, std::vector<void*>& owned, std::vector<Stage>& st,
@@ -1294,7 +1298,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       const int64_t nb = end - off;
       AdamArgs ar = a.adam;
       ar.P += off; ar.G += off; ar.M += off; ar.V += off; ar.T += off;
-      const W4Map wm = w4_map(h, g, off);
+      W4Map wm;
+      TD3_RC(w4_map(h, g, off, &wm));
       ar.grad_scale = 1.0f / (float)h->nranks;
       float* Gb = g.G + off;
       Stage x{std::string(tag) + "_" + std::to_string(b) + "_allreduce",
@@ -1412,7 +1417,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       float* Tp = g.T;
       const int64_t n = g.size;
       const float tau = (float)h->cfg.tau;
-      const W4Map wm = w4_map(h, g, 0);
+      W4Map wm;
+      TD3_RC(w4_map(h, g, 0, &wm));
       st.push_back({std::string(tag) + "_polyak", [=](hipStream_t s) { return launch_polyak_w4(Tp, Pp, n, tau, wm, s); },
                     0, "td3::polyak_w4_kernel"});
       return 0;
@@ -1424,7 +1430,7 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
       st.push_back({std::string(tag) + "_polyak", [=](hipStream_t s) { return launch_polyak_flat(Tp, Pp, n, tau, s); },
                     0, "td3::polyak_flat_kernel"});
     }
-    push_w4_pack(h, st, g, false, tag);
+    TD3_RC(push_w4_pack(h, st, g, false, tag));
     return 0;
   }
   if (dp) {
@@ -1456,7 +1462,8 @@ static int add_dw_stage(td3_handle* h, std::vector<void*>& owned, std::vector<St
     st.push_back({std::string(tag) + "_wn", [=](hipStream_t s) { return launch_wn(w, s); }, 0, "td3::wn_kernel"});
   } else if (dp) {
     const int64_t n = g.size;
-    const W4Map wm = w4_map(h, g, 0);
+    W4Map wm;
+    TD3_RC(w4_map(h, g, 0, &wm));
     st.push_back({std::string(tag) + "_adam",
                   [=](hipStream_t s) { return launch_adam_flat(aa, n, pol, s, &wm); }, 0,
                   "td3::adam_flat_kernel"});

@@ -20,9 +20,10 @@
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
-constexpr int NNET = 3, NOUT = 400, LDW = 512, MT = 16, NCT = 5, WK = 2, NW = NCT * WK;
+constexpr int REP = 4;                                              // networks streamed per workgroup
+constexpr int NNET = 3 * REP, NOUT = 400, LDW = 512, MT = 16, NCT = 5, WK = 2, NW = NCT * WK;
 constexpr int NTILE = (NOUT + 16 * NCT - 1) / (16 * NCT);          // 5 column tiles of 80
-constexpr int NWG = NNET * NTILE * MT;                              // 240
+constexpr int NWG = 3 * NTILE * MT;                                 // 240
 constexpr int NCH = LDW / 32, CPW = NCH / WK;                       // 16 chunks, 8 per wave
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -40,12 +41,14 @@ __global__ __launch_bounds__(64 * NW) void wstream(const float* W, float* out) {
   // consecutive tiles on one XCD (as xcd_tile): workgroup id b runs on XCD b % 8
   const int per = (NWG + 7) / 8, t = (b & 7) * per + (b >> 3);
   if (t >= NWG) return;
-  const int net = t / (NTILE * MT), r = t % (NTILE * MT), nt = r / MT;
+  const int net0 = t / (NTILE * MT), r = t % (NTILE * MT), nt = r / MT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j16 = lane & 15, g = lane >> 4;
   const int c = wave % NCT, kq = wave / NCT;
-  const float* Wn = W + (size_t)net * NOUT * LDW;
   const int n0 = nt * 16 * NCT + 16 * c;
   float4 v[2 * CPW];
+  float tot = 0.f;
+  for (int rep = 0; rep < REP; ++rep) {
+  const float* Wn = W + (size_t)(net0 + 3 * rep) * NOUT * LDW;
   if constexpr (PAT == 4 || PAT == 5) {
     // per wave: an LDS slot of R KB, refilled CPW*2/R times (rounds of R 1-KB instructions)
     extern __shared__ float4 sm4[];
@@ -64,13 +67,10 @@ __global__ __launch_bounds__(64 * NW) void wstream(const float* W, float* out) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       s += slot[lane * 4];
     }
-    out[(size_t)b * 64 * NW + threadIdx.x] = s;
-    return;
+    tot += s;
+    continue;
   }
-  if constexpr (PAT == 9) {
-    out[(size_t)b * 64 * NW + threadIdx.x] = 0.f;
-    return;
-  }
+  if constexpr (PAT == 9) break;
 #pragma unroll
   for (int q = 0; q < CPW; ++q) {
     if (PAT == 3 && q == CPW / 2) {
@@ -89,6 +89,10 @@ __global__ __launch_bounds__(64 * NW) void wstream(const float* W, float* out) {
       const float* p = Wn + (size_t)min(n0 + j16, NOUT - 1) * LDW + kb + 4 * g;
       v[2 * q] = ld4(p);
       v[2 * q + 1] = ld4(p + 16);
+    } else if (PAT == 6) {            // k-quad image of W: piece (n, j) at (j * NOUT + n) * 4
+      const float* p = Wn + ((size_t)((kb >> 2) + 2 * g) * NOUT + min(n0 + j16, NOUT - 1)) * 4;
+      v[2 * q] = ld4(p);
+      v[2 * q + 1] = ld4(p + 4 * NOUT);
     } else {
       const int row = lane >> 3, col = (lane & 7) * 4;
       v[2 * q] = ld4(Wn + (size_t)min(n0 + row, NOUT - 1) * LDW + kb + col);
@@ -98,7 +102,9 @@ __global__ __launch_bounds__(64 * NW) void wstream(const float* W, float* out) {
   float s = 0.f;
 #pragma unroll
   for (int q = 0; q < 2 * CPW; ++q) s += v[q].x + v[q].y + v[q].z + v[q].w;
-  out[(size_t)b * 64 * NW + threadIdx.x] = s;
+  tot += s;
+  }
+  out[(size_t)b * 64 * NW + threadIdx.x] = tot;
 }
 
 __global__ void touch(float* W, int n, float a) {
@@ -135,14 +141,15 @@ int main() {
   const int reps = 200;
   CK(hipFuncSetAttribute((const void*)wstream<4>, hipFuncAttributeMaxDynamicSharedMemorySize, NW * 8 * 1024));
   CK(hipFuncSetAttribute((const void*)wstream<5>, hipFuncAttributeMaxDynamicSharedMemorySize, NW * 8 * 1024));
-  printf("[%d wg x %d waves, %d KB per wg]\n", NWG, NW, CPW * 2 * 1024 * NW / 1024);
+  printf("[%d wg x %d waves, %d KB per wg]\n", NWG, NW, REP * CPW * 2 * 1024 * NW / 1024);
   for (int rnd = 0; rnd < 2; ++rnd) {
     for (int d = 0; d < 2; ++d) {
       const float t0 = run<0>(W, out, n, reps, d), t1 = run<1>(W, out, n, reps, d), t2 = run<2>(W, out, n, reps, d);
       const float t3 = run<3>(W, out, n, reps, d), t4 = run<4>(W, out, n, reps, d), t5 = run<5>(W, out, n, reps, d);
-      const float t9 = run<9>(W, out, n, reps, d);
+      const float t6 = run<6>(W, out, n, reps, d), t9 = run<9>(W, out, n, reps, d);
       printf("round %d %-18s: 8g-split %.2f  4g-contig %.2f  coalesced %.2f  8g-2rounds %.2f  ldsdma-r4 %.2f  "
-             "ldsdma-r8 %.2f  empty %.2f us\n", rnd, d ? "after a W rewrite" : "back to back", t0, t1, t2, t3, t4, t5, t9);
+             "ldsdma-r8 %.2f  kquad-image %.2f  empty %.2f us\n", rnd, d ? "after a W rewrite" : "back to back", t0, t1, t2, t3,
+             t4, t5, t6, t9);
     }
   }
   CK(hipFree(W));
