@@ -1202,8 +1202,13 @@ __device__ __forceinline__ void load_chunk(const GemmProb& P, float (&b)[16], in
     }
   } else {
     const float* wp = P.W + (size_t)kb * P.ldw + ncol;
+#ifdef TD3_KO_GEMM1       // knockout experiment (wrong results): no input-grad weight loads
+#pragma unroll
+    for (int s = 0; s < 16; ++s) b[s] = 1e-3f * s + 2e-3f * kb + 1e-4f * ncol;
+#else
 #pragma unroll
     for (int s = 0; s < 16; ++s) b[s] = gld(wp + (size_t)s * P.ldw);
+#endif
   }
 }
 
@@ -1233,8 +1238,13 @@ __device__ __forceinline__ void load_chunk16(const GemmProb& P, float (&b)[16], 
     }
   } else {
     const float* wp = P.W + (size_t)kb * P.ldw + ncol;
+#ifdef TD3_KO_GEMM1
+#pragma unroll
+    for (int s = 0; s < 8; ++s) b[s] = 1e-3f * s + 2e-3f * kb + 1e-4f * ncol;
+#else
 #pragma unroll
     for (int s = 0; s < 8; ++s) b[s] = gld(wp + (size_t)s * P.ldw);
+#endif
   }
 }
 
