@@ -3639,6 +3639,9 @@ int launch_l0r16(int nct, int wk, int gather, const GemmTable& t, int nblocks, i
   if (nct == 5 && wk == 2) {
     if (gather) hipLaunchKernelGGL((l0r16_kernel<5, 2, true>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
     else hipLaunchKernelGGL((l0r16_kernel<5, 2, false>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
+  } else if (nct == 6 && wk == 2) {
+    if (gather) hipLaunchKernelGGL((l0r16_kernel<6, 2, true>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
+    else hipLaunchKernelGGL((l0r16_kernel<6, 2, false>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
   } else if (nct == 2 && wk == 4) {
     if (gather) hipLaunchKernelGGL((l0r16_kernel<2, 4, true>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
     else hipLaunchKernelGGL((l0r16_kernel<2, 4, false>), grid, block, lds, s, nblocks, t.nprob, tb1, tb2, tb3, Bp, t, bump, bump_actor);
@@ -4019,7 +4022,8 @@ int kernels_init() {
                         (const void*)gemm_kernel<1, kWn4x2, kProCopy>, (const void*)gemm_kernel<1, kWn4x2, kProLNBwd>,
                         (const void*)gemm_kernel<1, kWn4x2, kProHeadBwd>,
                         (const void*)l0r16_kernel<5, 2, true>, (const void*)l0r16_kernel<5, 2, false>,
-                        (const void*)l0r16_kernel<2, 4, true>, (const void*)l0r16_kernel<2, 4, false>})
+                        (const void*)l0r16_kernel<2, 4, true>, (const void*)l0r16_kernel<2, 4, false>,
+                        (const void*)l0r16_kernel<6, 2, true>, (const void*)l0r16_kernel<6, 2, false>})
     TD3_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   return 0;
 }

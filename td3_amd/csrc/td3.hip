@@ -625,23 +625,34 @@ static bool can_fuse_l0(const std::vector<FwdItem>& items) {
 }
 
 // The fused layer-0 stage on 16-row tiles (l0r16_kernel) where it fills the chip in one round:
-// 80-column workgroups (10 waves) when 16-row x 80-column tiles of every network fit 256 workgroups
-// and 32-column ones (8 waves) would not, else 32-column workgroups when those fit (one network:
-// AF_fwd01), else none (the 32-row gemm_body stage).  B < 512 only; TD3_L0R16=0 turns it off.
+// 32-column workgroups (8 waves) when those fit 256 (one network: AF_fwd01), else 96-column ones
+// (12 waves) or 80-column ones (10 waves) when 16-row tiles of every network fit 256 workgroups,
+// else none (the 32-row gemm_body stage).  B < 512 only; TD3_L0R16=0 turns it off.
 static bool l0r16_config(const std::vector<FwdItem>& items, int Bp, int* nct, int* wk) {
   static const bool on = env_int("TD3_L0R16", 1) != 0;
   if (!on || Bp >= 512 || Bp % 16) return false;
-  int b80 = 0, b32 = 0;
+  int b80 = 0, b32 = 0, b96 = 0;
   for (auto& it : items) {
     const LinearL& L = it.net->lin[1];
     if (L.Kp > 512 || it.net->lin[0].Np != L.Kp) return false;
     b80 += (Bp / 16) * ((L.N + 79) / 80);
     b32 += (Bp / 16) * ((L.N + 31) / 32);
+    b96 += (Bp / 16) * ((L.N + 95) / 96);
   }
   static const int maxwg = env_int("TD3_L0R16_MAXWG", 256);
   if (b32 <= 256) {
     *nct = 2;
     *wk = 4;
+    return true;
+  }
+  // 96-column workgroups of 12 waves before 80-column ones of 10: three waves on every SIMD (10
+  // waves put three on two SIMDs and two on the others, whose layer-1 MFMA issue then waits for the
+  // first two) and the layer-0 tiles over 12 waves (C2 10.77 / 10.78 k -> 10.79 / 10.81 k, C1
+  // 10.95 / 10.97 k -> 10.98 / 10.99 k)
+  static const bool n96 = env_int("TD3_L0R16_N96", 1) != 0;
+  if (n96 && b96 <= 256) {
+    *nct = 6;
+    *wk = 2;
     return true;
   }
   if (b80 <= maxwg) {
