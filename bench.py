@@ -463,6 +463,13 @@ def run_rank(args):
 
     for _ in range(args.warmup):
         pol.train(rb, B)
+    # the timed runs hold Python's cyclic garbage collector (a collection inside a 2 ms driver-form
+    # run is a host stall the GPU waits behind); BENCH_GC=1 keeps it on
+    import gc
+    hold_gc = os.environ.get("BENCH_GC", "0") != "1"
+    if hold_gc:
+        gc.collect()
+        gc.disable()
     runs = []
     for _ in range(max(1, args.runs)):
         barrier_sync()
@@ -479,6 +486,8 @@ def run_rank(args):
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
         runs.append(dt)
+    if hold_gc:
+        gc.enable()
     dt = float(np.median(runs))
 
     rows, fam, roof, gat = None, None, None, None
