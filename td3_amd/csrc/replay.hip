@@ -30,8 +30,9 @@ namespace td3 {
 // Bytes moved per live row: rec*4 read + sum(len)*4 written (td3.hip input_from_ring).
 __device__ __forceinline__ int64_t gather_row_index(const GatherArgs& a, int row) {
   if (a.inject_idx) return a.inject_idx[row];
+  const uint64_t size = (uint64_t)*a.d_size;  // issued alongside the counter load
   const uint64_t step = a.ctr ? (uint64_t)(a.ctr->total_it + 1) : a.step;
-  return (int64_t)philox_index(a.seed, step, (uint32_t)row, (uint64_t)*a.d_size);
+  return (int64_t)philox_index(a.seed, step, (uint32_t)row, size);
 }
 
 template <bool STAGED>
@@ -45,9 +46,17 @@ __global__ __launch_bounds__(256) void gather_kernel(GatherArgs a) {
     float* lr = rec_lds[wave];
     if (live) {
       const int64_t idx = gather_row_index(a, row);
-      if (a.idx_out && lane == 0) a.idx_out[row] = idx;
       const float4* src = reinterpret_cast<const float4*>(a.data + (size_t)idx * a.rec);
-      for (int c = lane; c < (a.rec >> 2); c += 64) reinterpret_cast<float4*>(lr)[c] = src[c];
+      // All of the row's loads are issued before the first LDS write: a runtime-trip loop
+      // waits out one HBM round trip per 64 float4 (4 serial trips for a 3 KB record).
+      constexpr int kPer = kMaxRecord / 4 / 64;
+      const int n4 = a.rec >> 2;
+      float4 v[kPer];
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) v[i] = src[min(lane + 64 * i, n4 - 1)];  // unguarded: clamped
+#pragma unroll  // unguarded too (the slot holds kMaxRecord floats), or the loads sink into the guards
+      for (int i = 0; i < kPer; ++i) reinterpret_cast<float4*>(lr)[lane + 64 * i] = v[i];
+      if (a.idx_out && lane == 0) a.idx_out[row] = idx;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
