@@ -23,6 +23,7 @@
 // Compute dtype: fp32 everywhere.  Matrix products use v_mfma_f32_32x32x2_f32
 // (exact fp32 FMA chain, MI355X_MICROARCH.md § Matrix cores).
 #include <math.h>
+#include <stdlib.h>
 
 #include "dev.h"
 #include "kernels.h"
@@ -522,7 +523,41 @@ struct RowCtx {
 // exf[0]=max_action (1 for TD3_particles: tanh output, :68) exf[1]=policy_noise exf[2]=noise_clip
 constexpr int kHeadRegs = 8;   // head outputs kept in registers (wider heads loop)
 
-template <bool NORM>
+// Wide heads (action width > kHeadRegs; Humanoid: 17).  Requested block by block, the head weight
+// rows cost one dependent load round trip per kHeadRegs outputs (actor_head_bwd: a wave's chain
+// 8 us at Humanoid B = 1024, profiles/r05_timeline_humanoid.txt).  Instead the workgroup stages
+// every row once in (dynamic) LDS, all requests in one round trip, shared by its kWideRows rows
+// (RW: the launch's rows per workgroup); launch_rows sizes the LDS, launches the RW = kWideRows
+// variant and marks the problems (GemmProb::tile_begin = 1, otherwise unused by the row kernels).
+// The LDS rows are the same values, used in the same order: bit-identical results.
+constexpr int kWideStage = 16;   // float4 per thread: up to 64 KB staged by kWideRows waves
+constexpr int kWideRows = 4;     // rows (waves) per workgroup of the wide-head row launches
+// The row operands, re-defined after the stage: the wide and narrow paths' identical LayerNorm math
+// on them was hoisted above the branch, i.e. waited for the rows before the stage was requested
+__device__ __forceinline__ void opaque8(float (&v)[8]) {
+  asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+}
+__device__ __forceinline__ void opaque1(float& v) { asm volatile("" : "+v"(v)); }
+template <int NT>
+__device__ __forceinline__ void wide_stage(float4* dst, const float4* a, int n1, const float4* b, int n2) {
+  const int n = n1 + n2;
+  // surplus slots re-copy element `spare` (distinct per lane): unconditional loads and stores, so
+  // the compiler cannot sink the loads into per-slot branches (one round trip per slot)
+  const int spare = (int)threadIdx.x < n ? (int)threadIdx.x : 0;
+  float4 v[kWideStage];
+  int at[kWideStage];
+#pragma unroll
+  for (int i = 0; i < kWideStage; ++i) {
+    const int e = (int)threadIdx.x + NT * i;
+    at[i] = e < n ? e : spare;
+    v[i] = at[i] < n1 ? a[at[i]] : b[at[i] - n1];
+  }
+#pragma unroll
+  for (int i = 0; i < kWideStage; ++i) dst[at[i]] = v[i];
+  lds_barrier();
+}
+
+template <bool NORM, int RW = 1>
 __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx& c) {
   // every field in one scalar-load batch, and the step counter (Philox noise) requested with
   // the row: left alone, the compiler fetched fields where used (a chain of kernel-argument round
@@ -531,7 +566,7 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
                "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.exi[0]),
                "s"(P.exi[1]), "s"(P.exi[2]), "s"(P.exi[3]), "s"(P.exi[4]), "s"(P.exi[5]), "s"(P.exi[6]),
                "s"(P.exi[7]), "s"(P.exi[8]), "s"(P.exi[9]), "s"(P.exf[0]), "s"(P.exf[1]), "s"(P.exf[2]),
-               "s"(P.seed), "s"(P.ctr), "s"(P.B));
+               "s"(P.seed), "s"(P.ctr), "s"(P.B), "s"(P.tile_begin));
   const int K3 = P.exi[0], ld3 = P.exi[1], ldw4 = P.exi[2];
   const int ad = P.exi[5], sd = P.exi[6];
   const bool target = P.exi[8] != 0;
@@ -544,24 +579,49 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
   const int64_t* ctrp = &P.ctr->total_it + __builtin_amdgcn_mbcnt_lo(0u, 0u);
   const uint64_t stepv = (uint64_t)__hip_atomic_load(ctrp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float x[1][8], g[8], bb[8], mean[1], rstd[1];
-  float w4[kHeadRegs][8], b4v[kHeadRegs];
   rv_load(x[0], P.ex[0] + (size_t)c.row * ld3, ld3, c.lane);
   if (NORM) {
     rv_load(g, P.ex[1], ld3, c.lane);
     rv_load(bb, P.ex[2], ld3, c.lane);
   }
+  float nz = 0.f;
+  if (target && !P.exi[4] && c.lane < ad) nz = gld(P.ex[5] + ((size_t)c.row * P.exi[7] + c.lane));
+  float mine = 0.f;                       // lane o keeps head output o
+  if (RW > 1 && P.tile_begin) {           // wide head: W4's ad rows staged in LDS (wide_stage)
+    extern __shared__ float4 row_lds4[];
+    const float bl = gld(P.ex[4] + (c.lane < ad ? c.lane : 0));
+    wide_stage<64 * RW>(row_lds4, reinterpret_cast<const float4*>(P.ex[3]), ad * ldw4 / 4,
+               reinterpret_cast<const float4*>(P.ex[3]), 0);
+    const float* hw = reinterpret_cast<const float*>(row_lds4);
+    opaque8(x[0]); opaque8(g); opaque8(bb);
+    TL_MARK(5);
+    if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
+    for (int ob = 0; ob < ad; ob += kHeadRegs) {
+      float pb[kHeadRegs];
+#pragma unroll
+      for (int o = 0; o < kHeadRegs; ++o) {
+        float w[8];
+        rv_load_lds(w, hw + (size_t)(ob + o < ad ? ob + o : 0) * ldw4, ldw4, c.lane);
+        pb[o] = rv_pdot(x[0], w, K3, c.lane);
+      }
+#pragma unroll
+      for (int o = 0; o < kHeadRegs; ++o)
+        if (ob + o < ad) {
+          const float z = wsum(pb[o]) + bl;   // lane ob + o holds b4[ob + o]
+          if (c.lane == ob + o) mine = z;
+        }
+    }
+  } else {
+  float w4[kHeadRegs][8], b4v[kHeadRegs];
 #pragma unroll
   for (int o = 0; o < kHeadRegs; ++o) {
     const int oo = o < ad ? o : 0;
     rv_load(w4[o], P.ex[3] + (size_t)oo * ldw4, ldw4, c.lane);
     b4v[o] = gld(P.ex[4] + oo);
   }
-  float nz = 0.f;
-  if (target && !P.exi[4] && c.lane < ad) nz = gld(P.ex[5] + ((size_t)c.row * P.exi[7] + c.lane));
   TL_MARK(5);
   TL_FINE(6);
   if (NORM) ln_fwd_rows<1>(x, g, bb, K3, c.lane, mean, rstd);
-  float mine = 0.f;                       // lane o keeps head output o
   float part[kHeadRegs];
 #pragma unroll
   for (int o = 0; o < kHeadRegs; ++o) part[o] = rv_pdot(x[0], w4[o], K3, c.lane);
@@ -571,8 +631,8 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
       const float z = wsum(part[o]) + b4v[o];
       if (c.lane == o) mine = z;
     }
-  // wide action spaces (Humanoid: 17): further blocks of kHeadRegs outputs, each block's W4 rows
-  // and biases requested in one batch (one load round trip per block)
+  // wide action spaces without the LDS stage: further blocks of kHeadRegs outputs, each block's
+  // W4 rows and biases requested in one batch (one load round trip per block)
   for (int ob = kHeadRegs; ob < ad; ob += kHeadRegs) {
     float wb[kHeadRegs][8], bv[kHeadRegs];
 #pragma unroll
@@ -590,6 +650,7 @@ __device__ __forceinline__ void row_policy_head(const GemmProb& P, const RowCtx&
         const float z = wsum(pb[o]) + bv[o];
         if (c.lane == ob + o) mine = z;
       }
+  }
   }
   if (!target) {
     if (NORM) rv_store(P.ex[8] + (size_t)c.row * ld3, ld3, c.lane, x[0]);
@@ -743,7 +804,7 @@ __device__ __forceinline__ void head_cols(const float* W, int ldw, int s0, int l
 // out: ex[10]=dZ4 actor (ld 32) ex[11]=dU3 actor  Aout=dZ3 actor
 // exi[0]=K0 exi[1]=ld0 exi[2]=ldw1 exi[3]=sd exi[4]=ad exi[5]=K3 exi[6]=ld3 exi[7]=ldw4
 // exf[0]=max_action
-template <bool NORM>
+template <bool NORM, int RW = 1>
 __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowCtx& c) {
   // every field in one scalar-load batch (left alone, the compiler requested them where used, in
   // dependent kernel-argument round trips between the row's loads)
@@ -751,7 +812,7 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
                "s"(P.ex[6]), "s"(P.ex[7]), "s"(P.ex[8]), "s"(P.ex[9]), "s"(P.ex[10]), "s"(P.ex[11]),
                "s"(P.ex[12]), "s"(P.exi[0]), "s"(P.exi[1]), "s"(P.exi[2]), "s"(P.exi[3]), "s"(P.exi[4]),
                "s"(P.exi[5]), "s"(P.exi[6]), "s"(P.exi[7]), "s"(P.exi[8]), "s"(P.exf[0]), "s"(P.Aout),
-               "s"(P.ldao), "s"(P.B));
+               "s"(P.ldao), "s"(P.B), "s"(P.tile_begin));
   const int K0 = P.exi[0], ld0 = P.exi[1], ldw1 = P.exi[2], sd = P.exi[3], ad = P.exi[4];
   const int K3 = P.exi[5], ld3 = P.exi[6], ldw4 = P.exi[7];
   const float ma = P.exf[0];
@@ -775,6 +836,46 @@ __device__ __forceinline__ void row_actor_head_bwd(const GemmProb& P, const RowC
   // W1[:, sd+o], the action columns: rows of the transposed copy when the step keeps one (ex[12],
   // row length exi[8]: coalesced, the same elements per lane), else strided column reads
   const float* w1t = P.ex[12];
+  if (RW > 1 && P.tile_begin) {     // wide head (wide_stage): the transposed W1 rows, then W4's, in LDS
+    extern __shared__ float4 row_lds4[];
+    const int n1 = ad * P.exi[8] / 4;
+    wide_stage<64 * RW>(row_lds4, reinterpret_cast<const float4*>(w1t), n1, reinterpret_cast<const float4*>(P.ex[6]),
+               ad * ldw4 / 4);
+    const float* hw1 = reinterpret_cast<const float*>(row_lds4);
+    const float* hw4 = hw1 + (size_t)4 * n1;
+    opaque8(gu0[0]); opaque8(h0[0]); opaque8(h3[0]); opaque8(g0); opaque8(g3);
+    opaque1(mn0[0]); opaque1(rs0[0]); opaque1(mn3[0]); opaque1(rs3[0]);
+    ln_bwd_rows<1>(gu0, h0, g0, mn0, rs0, K0, c.lane, NORM);       // dZ0 of Q1 (pads -> 0)
+    const bool live = c.row < P.B;
+    float gu3[1][8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) gu3[0][jj] = 0.f;
+    for (int ob = 0; ob < ad; ob += kHeadRegs) {
+      float pb[kHeadRegs];
+#pragma unroll
+      for (int o = 0; o < kHeadRegs; ++o) {
+        float w[8];
+        rv_load_lds(w, hw1 + (size_t)(ob + o < ad ? ob + o : 0) * P.exi[8], K0, c.lane);
+        pb[o] = rv_pdot(gu0[0], w, K0, c.lane);
+      }
+#pragma unroll
+      for (int o = 0; o < kHeadRegs; ++o)
+        if (ob + o < ad) {
+          const float ga = wsum(pb[o]);                               // dL/da_o
+          const float t = __shfl(tl, ob + o, 64);
+          const float gz4 = live ? (ga * ma) * (1.f - t * t) : 0.f;   // max_action*tanh bwd
+          if (c.lane == 0) gst(P.ex[10] + ((size_t)c.row * 32 + ob + o), gz4);
+          float w4r[8];
+          rv_load_lds(w4r, hw4 + (size_t)(ob + o) * ldw4, ldw4, c.lane);
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) gu3[0][jj] += gz4 * w4r[jj];
+        }
+    }
+    rv_store(P.ex[11] + (size_t)c.row * ld3, ld3, c.lane, gu3[0]);
+    ln_bwd_rows<1>(gu3, h3, g3, mn3, rs3, K3, c.lane, NORM);        // dZ3 of the actor
+    rv_store(P.Aout + (size_t)c.row * P.ldao, P.ldao, c.lane, gu3[0]);
+    return;
+  }
   if (w1t) {
 #pragma unroll
     for (int o = 0; o < kHeadRegs; ++o) rv_load(w1[o], w1t + (size_t)(o < ad ? o : 0) * P.exi[8], K0, c.lane);
@@ -1130,12 +1231,12 @@ __device__ __forceinline__ void row_lnbwd(const GemmProb& P, const RowCtx& c) {
   rv_store(P.ex[4] + (size_t)c.row * ld, ld, c.lane, gu[0]);
 }
 
-template <int KIND, bool NORM>
+template <int KIND, bool NORM, int RW>
 __device__ __forceinline__ void row_dispatch(const GemmProb& P, const RowCtx& c) {
-  if constexpr (KIND == kRowPolicyHead) row_policy_head<NORM>(P, c);
+  if constexpr (KIND == kRowPolicyHead) row_policy_head<NORM, RW>(P, c);
   else if constexpr (KIND == kRowCriticLoss) row_critic_loss<NORM>(P, c);
   else if constexpr (KIND == kRowActorLoss) row_actor_loss<NORM>(P, c);
-  else if constexpr (KIND == kRowActorHeadBwd) row_actor_head_bwd<NORM>(P, c);
+  else if constexpr (KIND == kRowActorHeadBwd) row_actor_head_bwd<NORM, RW>(P, c);
   else if constexpr (KIND == kRowCriticLossP) row_critic_loss_p<NORM>(P, c);
   else if constexpr (KIND == kRowActorLossP) row_actor_loss_p<NORM>(P, c);
   else if constexpr (KIND == kRowActorHeadBwdP) row_actor_head_bwd_p<NORM>(P, c);
@@ -1144,26 +1245,26 @@ __device__ __forceinline__ void row_dispatch(const GemmProb& P, const RowCtx& c)
   else if constexpr (KIND == kRowLnBwd) row_lnbwd<NORM>(P, c);
 }
 
-template <int KIND, bool NORM>
-__global__ __launch_bounds__(64 * kRowWaves) void row_kernel(int Bp, GemmTable tab) {   // Bp first: preloaded
+template <int KIND, bool NORM, int RW = kRowWaves>
+__global__ __launch_bounds__(64 * RW) void row_kernel(int Bp, GemmTable tab) {   // Bp first: preloaded
   const GemmProb& P = tab.p[blockIdx.y];
-  // grid.x = Bp / kRowWaves exactly (launch_rows): every wave owns a row, no bounds check (which would put
+  // grid.x = Bp / RW exactly (launch_rows): every wave owns a row, no bounds check (which would put
   // a kernel-argument round trip ahead of the row's loads)
-  const RowCtx c{(int)(blockIdx.x * kRowWaves + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
+  const RowCtx c{(int)(blockIdx.x * RW + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
   TL_MARK(0);
-  row_dispatch<KIND, NORM>(P, c);
+  row_dispatch<KIND, NORM, RW>(P, c);
   TL_MARK(3);
 }
 
 // Two independent row stages in one launch (problems [0, n1) of kind K1, the rest K2): the
 // branch is on blockIdx.y, uniform per workgroup.
-template <int K1, int K2, bool NORM>
-__global__ __launch_bounds__(64 * kRowWaves) void row_kernel2(int Bp, int n1, GemmTable tab) {
+template <int K1, int K2, bool NORM, int RW = kRowWaves>
+__global__ __launch_bounds__(64 * RW) void row_kernel2(int Bp, int n1, GemmTable tab) {
   const GemmProb& P = tab.p[blockIdx.y];
-  const RowCtx c{(int)(blockIdx.x * kRowWaves + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
+  const RowCtx c{(int)(blockIdx.x * RW + (threadIdx.x >> 6)), (int)(threadIdx.x & 63), Bp};
   TL_MARK(0);
-  if ((int)blockIdx.y < n1) row_dispatch<K1, NORM>(P, c);
-  else row_dispatch<K2, NORM>(P, c);
+  if ((int)blockIdx.y < n1) row_dispatch<K1, NORM, RW>(P, c);
+  else row_dispatch<K2, NORM, RW>(P, c);
   TL_MARK(3);
 }
 
@@ -3666,15 +3767,55 @@ int launch_gemm(int mode, int wn, int pro, const GemmTable& t, int nblocks, int 
   return 0;
 }
 
+// The wide-head LDS stage (wide_stage) of row problem p of kind `kind`: its bytes, or 0 when the
+// head is narrow (<= kHeadRegs outputs) or its rows cannot be staged (alignment, > 64 KB, no
+// transposed W1 copy) and the kernel requests them block by block.
+static int wide_head_bytes(int kind, const GemmProb& p) {
+  const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  size_t n = 0;
+  if (kind == kRowPolicyHead) {
+    const int ad = p.exi[5], ldw4 = p.exi[2];
+    if (ad <= kHeadRegs || ldw4 % 4 || !al16(p.ex[3])) return 0;
+    n = (size_t)ad * ldw4;
+  } else if (kind == kRowActorHeadBwd) {
+    const int ad = p.exi[4], ldw4 = p.exi[7], ld1 = p.exi[8];
+    if (ad <= kHeadRegs || !p.ex[12] || ld1 % 4 || ldw4 % 4 || !al16(p.ex[12]) || !al16(p.ex[6])) return 0;
+    n = (size_t)ad * (ld1 + ldw4);
+  }
+  return n * 4 <= (size_t)kWideStage * 64 * kWideRows * 16 ? (int)(n * 4) : 0;
+}
+
+// Marks the wide problems (GemmProb::tile_begin, read by the row kernels as the wide flag) of a
+// row table whose problems [0, n1) are of kind k1 and the rest of kind k2; returns the LDS bytes.
+// TD3_WIDE_HEADS=0 keeps the block-by-block requests (read per launch: the bit-identity test flips it)
+static int mark_wide(GemmTable& d, int k1, int k2, int n1) {
+  const char* e = getenv("TD3_WIDE_HEADS");
+  const bool on = !e || atoi(e) != 0;
+  int lds = 0;
+  for (int i = 0; i < d.nprob; ++i) {
+    const int b = on ? wide_head_bytes(i < n1 ? k1 : k2, d.p[i]) : 0;
+    d.p[i].tile_begin = b > 0;
+    lds = std::max(lds, b);
+  }
+  return lds;
+}
+
 template <bool NORM>
-static void launch_rows_t(int kind, const GemmTable& d, int Bp, hipStream_t s) {
-  const dim3 grid(Bp / kRowWaves, d.nprob);
+static void launch_rows_t(int kind, const GemmTable& d0, int Bp, hipStream_t s) {
+  const dim3 grid(Bp / kRowWaves, d0.nprob);
+  GemmTable d = d0;
+  const int lds = mark_wide(d, kind, kind, d.nprob);
+  const dim3 wgrid(Bp / kWideRows, d0.nprob), wblock(64 * kWideRows);
   switch (kind) {
-    case kRowPolicyHead: hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
+    case kRowPolicyHead:
+      if (lds) hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM, kWideRows>), wgrid, wblock, lds, s, Bp, d);
+      else hipLaunchKernelGGL((row_kernel<kRowPolicyHead, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
+      break;
     case kRowCriticLoss: hipLaunchKernelGGL((row_kernel<kRowCriticLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
     case kRowActorLoss: hipLaunchKernelGGL((row_kernel<kRowActorLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d); break;
     case kRowActorHeadBwd:
-      hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
+      if (lds) hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM, kWideRows>), wgrid, wblock, lds, s, Bp, d);
+      else hipLaunchKernelGGL((row_kernel<kRowActorHeadBwd, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
       break;
     case kRowCriticLossP:
       hipLaunchKernelGGL((row_kernel<kRowCriticLossP, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, d);
@@ -3701,9 +3842,14 @@ int launch_rows(int kind, const GemmTable& d, int Bp, hipStream_t s) {
 }
 
 template <bool NORM>
-static int launch_rows2_t(int k1, int k2, int n1, const GemmTable& d, int Bp, hipStream_t s) {
-  const dim3 grid(Bp / kRowWaves, d.nprob);
-  if (k1 == kRowPolicyHead && k2 == kRowUnitLoss)
+static int launch_rows2_t(int k1, int k2, int n1, const GemmTable& d0, int Bp, hipStream_t s) {
+  const dim3 grid(Bp / kRowWaves, d0.nprob);
+  GemmTable d = d0;
+  const int lds = mark_wide(d, k1, k2, n1);
+  if (k1 == kRowPolicyHead && k2 == kRowUnitLoss && lds)
+    hipLaunchKernelGGL((row_kernel2<kRowPolicyHead, kRowUnitLoss, NORM, kWideRows>), dim3(Bp / kWideRows, d0.nprob),
+                       dim3(64 * kWideRows), lds, s, Bp, n1, d);
+  else if (k1 == kRowPolicyHead && k2 == kRowUnitLoss)
     hipLaunchKernelGGL((row_kernel2<kRowPolicyHead, kRowUnitLoss, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, n1, d);
   else if (k1 == kRowTargetLoss && k2 == kRowLnBwd)
     hipLaunchKernelGGL((row_kernel2<kRowTargetLoss, kRowLnBwd, NORM>), grid, dim3(64 * kRowWaves), 0, s, Bp, n1, d);
